@@ -1,0 +1,260 @@
+#!/usr/bin/env python
+"""bench.py — SGHMC steps/s + predictive samples/s of the L=3, RF=1024 DGP (BASELINE config 2).
+
+A "step" is one DGP_RF.sgmcmc_update (models/dgp.py:184-216): on-device minibatch of B=200 rows
+from the device-resident N=1e6 x 8 dataset, forward through 3 RBF-RF layers, Gaussian
+likelihood, analytic backward, SGHMC update with Philox noise — one chain per GPU (weak scaling,
+chain-parallel).  A "predictive sample" is the full forward of the N_t=1e5 test set for one
+posterior sample + log p + se + the online log-sum-exp accumulation (utils_training.py:79-85).
+
+  python bench.py [--gpus N --steps K --warmup W]
+  python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+      --master-port P bench.py --gpus N --steps K --warmup W
+Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "dgp-rf-mcmc_amd")
+for _p in (ROOT, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "SGHMC steps/sec + predictive samples/sec, L=3 RF=1024 DGP, 1/2/4/8 GPU"
+FP32_MFMA_PEAK = 157.3e12   # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 dense peak (FLOP/s)
+HBM_PEAK = 8.0e12           # MI355X_MICROARCH.md: HBM3E spec (B/s)
+
+CFG = dict(L=3, n_rf=1024, n_gp=[8, 8, 1], D=8, N=1_000_000, B=200, N_test=100_000,
+           variance=0.1, lr=0.01, beta=0.9, T=1.0)
+
+
+def step_flops(B, d, R, P, g):
+    """per-kernel algorithmic FLOPs of one step (per layer)."""
+    fwd = [2 * B * (d[l] * R[l] + P[l] * g[l]) for l in range(len(d))]
+    bwd = [2 * B * P[l] * g[l] + (2 * B * (P[l] * g[l] + R[l] * d[l]) if l > 0 else 0)
+           for l in range(len(d))]
+    return fwd, bwd
+
+
+def pred_flops(n, d, R, P, g):
+    return n * sum(2 * (d[l] * R[l] + P[l] * g[l]) for l in range(len(d)))
+
+
+def cpu_baseline(seconds):
+    """The reference algorithm, op for op, on the host (oracle/dgp_oracle.py in float32 numpy):
+    TensorFlow is not installed here or on the GPU box, so this restatement is the CPU proxy."""
+    from oracle import dgp_oracle as O
+    rng = np.random.default_rng(0)
+    f32 = np.float32
+    d, R, g = [8, 8, 8], CFG["n_rf"], CFG["n_gp"]
+    p = O.Params(8, 1, [R] * 3, g, ["RBF"] * 3, "gaussian", False, rng=rng,
+                 lik_log_var=np.log(CFG["variance"]), dtype=np.float32)
+    n_data = 200_000   # host copy of the synthetic regression data (same distribution)
+    X = rng.standard_normal((n_data, 8)).astype(f32)
+    a = rng.standard_normal((8, 1)).astype(f32) / f32(np.sqrt(8))
+    Y = (np.sin(X @ a) + f32(0.1) * rng.standard_normal((n_data, 1)).astype(f32)).astype(f32)
+    Y = ((Y - Y.mean()) / Y.std()).astype(f32)
+    m = [rng.standard_normal(w.shape).astype(f32) for w in p.W]
+    N, B = CFG["N"], CFG["B"]
+    steps, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        idx = rng.integers(0, n_data, B)
+        xi = [rng.standard_normal(w.shape).astype(f32) for w in p.W]
+        m = O.sgmcmc_step(p, m, X[idx], Y[idx], f32(N), f32(CFG["lr"]), f32(CFG["beta"]),
+                          f32(CFG["T"]), [f32(1.0)] * 3, xi)
+        steps += 1
+    step_rate = steps / (time.perf_counter() - t0)
+    # predictive: forward + log p + se of a 10,000-row slice, scaled to N_test = 1e5 rows
+    Xt = rng.standard_normal((10_000, 8)).astype(f32)
+    Yt = rng.standard_normal((10_000, 1)).astype(f32)
+    reps, t0 = 0, time.perf_counter()
+    while reps < 3 or time.perf_counter() - t0 < min(5.0, seconds / 3):
+        O.eval_log_likelihood_and_se(p, Xt, Yt)
+        reps += 1
+    pred_rate = reps / (time.perf_counter() - t0) / (CFG["N_test"] / 10_000)
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    return {"value": round(step_rate, 2), "unit": "steps/s", "cores": threads, "kind": "port",
+            "sample": f"{steps} SGHMC steps of config 2 (B=200, L=3, n_rf=1024, float32 numpy "
+                      f"op-for-op restatement of models/dgp.py:184-216, injected N(0,1) noise); "
+                      f"predictive on a 10k-row slice scaled to 1e5 rows",
+            "predictive_samples_per_s": round(pred_rate, 4),
+            "note": "BLAS matmuls use the listed threads; numpy elementwise/trig is single-threaded"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10000)
+    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--steps-per-graph", type=int, default=100)
+    ap.add_argument("--pred-samples", type=int, default=20)
+    ap.add_argument("--multi-chains", type=int, default=64)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--profile-reps", type=int, default=200)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from dgprf import engine as E
+    from dgprf import _native as N
+    from dgprf.data import regression_data
+    from dgprf.distributed import rank_seed
+    from dgprf.predictive import PredictiveLSE
+    from likelihoods import Gaussian
+    from models.regression_model import RegressionDGP
+
+    def barrier_sync():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    def max_over_ranks(x):
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    N_, B = CFG["N"], CFG["B"]
+    X, Y, a = regression_data(N_, CFG["D"], seed=0, device=dev)
+    Xt, Yt, _ = regression_data(CFG["N_test"], CFG["D"], seed=1, device=dev, a=a)
+    E.set_seed(rank_seed(2, rank))
+    model = RegressionDGP(CFG["D"], 1, n_hidden_layers=CFG["L"], n_rf=CFG["n_rf"],
+                          n_gp=CFG["n_gp"], likelihood=Gaussian(variance=CFG["variance"]))
+    model.precond_update(None, N_, precond_type="identity")
+    run = dict(batch_size=B, lr=CFG["lr"], momentum_decay=CFG["beta"], temperature=CFG["T"],
+               steps_per_graph=args.steps_per_graph, perm_seed=rank_seed(0, rank))
+
+    # ---------------- SGHMC steps (graph-replayed, on-device minibatching)
+    model.run_sgmcmc(X, Y, N_, args.warmup, **run)
+    barrier_sync()
+    t0 = time.perf_counter()
+    model.run_sgmcmc(X, Y, N_, args.steps, **run)
+    barrier_sync()
+    t_steps = max_over_ranks(time.perf_counter() - t0)
+    assert torch.isfinite(model._engine.theta).all(), "chain diverged"
+    steps_per_s = world * args.steps / t_steps
+
+    # ---------------- predictive samples (full test forward + log p + se + LSE fold)
+    acc = PredictiveLSE(model._engine, Xt, Yt)
+    acc.add_sample()
+    acc.add_sample()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    barrier_sync()
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(args.pred_samples):
+        acc.add_sample(build=False)
+    ev1.record()
+    ll, rmse = acc.finalize(y_std=1.0)
+    barrier_sync()
+    t_pred = max_over_ranks(time.perf_counter() - t0)
+    pred_kernel_ms = ev0.elapsed_time(ev1) / args.pred_samples
+    pred_per_s = world * args.pred_samples / t_pred
+
+    # ---------------- per-kernel device times (hipEvents on the launch stream) -> roofline
+    eng = model._engine
+    pl = eng.layout
+    d, R, P, g = (list(pl.d[:3]), list(pl.n_rf[:3]), list(pl.P[:3]), list(pl.n_gp[:3]))
+    prof = eng.profile_step(X, Y, B, N_, CFG["lr"], CFG["beta"], CFG["T"], reps=args.profile_reps)
+    fwd_f, bwd_f = step_flops(B, d, R, P, g)
+    per_name = {
+        "k_step_fwd": (sum(prof["fwd"]) / 3, sum(fwd_f) / 3, 3),
+        "k_step_bwd": (sum(prof["bwd"]) / 3, sum(bwd_f) / 3, 3),
+    }
+    upd_bytes = 4 * pl.w_total * (pl.n_row_tiles + 2 + 2 + 2)  # gW partials + theta/mom r/w
+    dom = max(per_name, key=lambda k: per_name[k][0] * per_name[k][2])
+    ms_dom, fl_dom, _ = per_name[dom]
+    roof = {"kernel": dom + "<SMALLD=true>", "bound": "mfma",
+            "achieved": round(fl_dom / (ms_dom * 1e-3) / 1e12, 6),
+            "peak": FP32_MFMA_PEAK / 1e12, "unit": "TFLOP/s",
+            "frac": round(fl_dom / (ms_dom * 1e-3) / FP32_MFMA_PEAK, 8), "traffic": None,
+            "avg_launch_us": round(ms_dom * 1e3, 3),
+            "flops_per_launch": int(fl_dom),
+            "step_kernel_us": {"fwd": [round(x * 1e3, 3) for x in prof["fwd"]],
+                               "bwd": [round(x * 1e3, 3) for x in prof["bwd"]],
+                               "update": round(prof["update"] * 1e3, 3)},
+            "update_hbm_GBps": round(upd_bytes / (prof["update"] * 1e-3) / 1e9, 2),
+            "regime": "latency-bound at B=200: 51.6 MFLOP/step; see DESIGN.md"}
+    fp = pred_flops(CFG["N_test"], d, R, P, g)
+    roof_pred = {"kernel": "k_forward_rows<SMALLD=true>", "bound": "mfma",
+                 "achieved": round(fp / (pred_kernel_ms * 1e-3) / 1e12, 4),
+                 "peak": FP32_MFMA_PEAK / 1e12, "unit": "TFLOP/s",
+                 "frac": round(fp / (pred_kernel_ms * 1e-3) / FP32_MFMA_PEAK, 5),
+                 "traffic": None, "avg_launch_us": round(pred_kernel_ms * 1e3, 2),
+                 "flops_per_launch": int(fp)}
+
+    # ---------------- many chains per GPU (aggregate chain-steps/s; extra, not `value`)
+    multi = None
+    if args.multi_chains > 1:
+        spec = eng.spec
+        me = E.Engine(spec, args.multi_chains, seed=rank_seed(3, rank))
+        me.z.copy_(eng.z)
+        me.hyp.copy_(eng.hyp)
+        E.normal(None, N.RNG_W, out=me.theta)
+        me.init_moments()
+        me.lik_log_var_source = eng.lik_log_var_source
+        me.build_omega()
+        k_m = max(50, args.steps // 20)
+        gph = me.graph(X, Y, B, N_, CFG["lr"], CFG["beta"], CFG["T"], 50)
+        gph.launch()
+        barrier_sync()
+        t0 = time.perf_counter()
+        for _ in range(k_m // 50):
+            gph.launch()
+        barrier_sync()
+        t_m = max_over_ranks(time.perf_counter() - t0)
+        multi = {"chains_per_gpu": args.multi_chains,
+                 "chain_steps_per_s": round(world * args.multi_chains * (k_m // 50) * 50 / t_m, 1),
+                 "ms_per_step_all_chains": round(t_m * 1e3 / ((k_m // 50) * 50), 4)}
+        del me, gph
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(steps_per_s, 2), "unit": "steps/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(t_steps * 1e3 / args.steps, 5), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic config 2: X~N(0,I) [1e6,8] seed 0, y=sin(Xa)+0.1eps standardized; "
+                    "test [1e5,8] seed 1; random-init weights (Philox)",
+            "config": {"workload": "config2: 3-layer RBF-RF DGP, n_rf=1024 (Phi 2048), g=[8,8,1], "
+                                   "D=8, N=1e6, B=200, Gaussian s2=0.1, SGHMC lr=0.01 beta=0.9 T=1, "
+                                   "W-only, identity preconditioner",
+                       "chains_per_gpu": 1, "steps_per_graph": args.steps_per_graph,
+                       "parallelism": f"chain-parallel x{world} (independent chains, RCCL "
+                                      "all-gather of predictive accumulators only)"},
+            "predictive_samples_per_s": round(pred_per_s, 3),
+            "predictive": {"n_test": CFG["N_test"], "samples": args.pred_samples,
+                           "test_loglik": round(ll, 6), "test_rmse": round(rmse, 6),
+                           "ms_per_sample": round(t_pred * 1e3 / args.pred_samples, 4)},
+            "roofline": roof, "roofline_predictive": roof_pred, "cpu_baseline": cpu,
+            "multi_chain": multi, "device": torch.cuda.get_device_name(dev),
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

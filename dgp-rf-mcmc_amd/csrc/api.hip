@@ -1,0 +1,436 @@
+// api.hip — extern "C" entry points of libdgprf.so (declared in include/dgprf.h).
+//
+// Host-side validation and planning mirror the reference's constructor and assertions
+// (models/dgp.py:34-52, 74-115; kernels/RBF.py:19-27; kernels/arc_cosine.py:13-16): configuration
+// errors are reported as return codes before anything is enqueued.
+#include <cstring>
+#include <new>
+
+#include "dgprf_internal.h"
+
+namespace {
+
+inline int64_t align4(int64_t x) { return (x + 3) & ~int64_t(3); }
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+int hip_rc(hipError_t e) { return e == hipSuccess ? DGPRF_OK : DGPRF_E_HIP; }
+
+StepDev make_step_dev(const dgprf_plan_t& pl, const dgprf_chain_t& ch, const dgprf_batch_t& b,
+                      int32_t step_offset) {
+  StepDev sd;
+  sd.theta = ch.theta;
+  sd.mom = ch.mom;
+  sd.omega = ch.omega;
+  sd.der = ch.der;
+  sd.mass = ch.mass;
+  sd.ws = ch.ws;
+  sd.step = ch.step;
+  sd.grad_out = nullptr;
+  sd.seed = ch.seed;
+  sd.bd.X = b.X;
+  sd.bd.Y = b.Y;
+  sd.bd.idx = b.idx;
+  sd.bd.n_data = b.n_data;
+  sd.bd.iters = b.iters_per_epoch;
+  sd.bd.perm_seed = b.perm_seed;
+  sd.bd.y_cols = b.y_cols;
+  sd.bd.mode = b.mode;
+  sd.step_offset = step_offset;
+  (void)pl;
+  return sd;
+}
+
+UpdateDev make_update_dev(const dgprf_step_t& st) {
+  UpdateDev ud;
+  ud.lr = st.lr;
+  ud.beta = st.momentum_decay;
+  ud.temperature = st.temperature;
+  ud.data_size = st.data_size;
+  ud.resample = st.resample_moments;
+  ud.schedule = st.schedule;
+  ud.grad_only = st.grad_only;
+  ud.resample_head = st.resample_in_cycle_head;
+  ud.start_step = st.start_step;
+  ud.cycle_length = st.cycle_length > 0 ? st.cycle_length : 1;
+  ud.xi = st.xi;
+  ud.xi_resample = st.xi_resample;
+  return ud;
+}
+
+int check_plan(const dgprf_plan_t* pl) {
+  if (!pl) return DGPRF_E_ARG;
+  if (pl->initialised != 1) return DGPRF_E_PLAN;
+  return DGPRF_OK;
+}
+
+int check_chain(const dgprf_chain_t* ch) {
+  if (!ch || !ch->theta || !ch->mom || !ch->omega || !ch->der || !ch->mass || !ch->ws || !ch->step)
+    return DGPRF_E_ARG;
+  return DGPRF_OK;
+}
+
+int check_batch(const dgprf_plan_t& pl, const dgprf_batch_t* b) {
+  if (!b || !b->X || !b->Y || b->y_cols < 1) return DGPRF_E_ARG;
+  if (b->mode == DGPRF_BATCH_DIRECT) {
+    if (b->n_data < pl.batch) return DGPRF_E_SHAPE;
+  } else if (b->mode == DGPRF_BATCH_INDEXED) {
+    if (!b->idx) return DGPRF_E_ARG;
+  } else if (b->mode == DGPRF_BATCH_EPOCH) {
+    if (b->iters_per_epoch < 1 || b->iters_per_epoch * (int64_t)pl.batch > b->n_data ||
+        b->n_data > (int64_t)0xFFFFFFFFll)
+      return DGPRF_E_SHAPE;
+  } else {
+    return DGPRF_E_ARG;
+  }
+  if (pl.likelihood == DGPRF_LIK_GAUSSIAN && b->y_cols < pl.n_gp[pl.n_layers - 1]) return DGPRF_E_SHAPE;
+  return DGPRF_OK;
+}
+
+int check_step(const dgprf_step_t* st) {
+  if (!st) return DGPRF_E_ARG;
+  if (!(st->data_size > 0.f)) return DGPRF_E_ARG;
+  if (st->schedule != DGPRF_SCHED_CONST && st->schedule != DGPRF_SCHED_CYCLICAL) return DGPRF_E_ARG;
+  return DGPRF_OK;
+}
+
+// fwd for every layer, bwd in reverse, then the fused update (or gradient reduction).
+hipError_t enqueue_step(const dgprf_plan_t& pl, const StepDev& sd, const UpdateDev& ud,
+                        hipStream_t s) {
+  hipError_t e = hipSuccess;
+  for (int l = 0; l < pl.n_layers && e == hipSuccess; ++l) e = dgprf::launch_step_fwd(pl, sd, l, s);
+  for (int l = pl.n_layers - 1; l >= 0 && e == hipSuccess; --l)
+    e = dgprf::launch_step_bwd(pl, sd, l, s);
+  if (e == hipSuccess) e = dgprf::launch_step_update(pl, sd, ud, nullptr, s);
+  return e;
+}
+
+}  // namespace
+
+struct dgprf_graph {
+  hipGraph_t graph;
+  hipGraphExec_t exec;
+};
+
+extern "C" {
+
+int dgprf_abi_version(void) { return DGPRF_ABI_VERSION; }
+
+const char* dgprf_error_string(int code) {
+  switch (code) {
+    case DGPRF_OK: return "ok";
+    case DGPRF_E_ARG: return "invalid argument (null pointer or bad scalar)";
+    case DGPRF_E_SHAPE: return "unsupported shape";
+    case DGPRF_E_HIP: return "HIP runtime error";
+    case DGPRF_E_PLAN: return "plan not initialised (call dgprf_plan_init)";
+    default: return "unknown error";
+  }
+}
+
+int dgprf_plan_init(dgprf_plan_t* pl) {
+  if (!pl) return DGPRF_E_ARG;
+  pl->initialised = 0;
+  const int L = pl->n_layers;
+  if (L < 1 || L > DGPRF_MAX_LAYERS) return DGPRF_E_SHAPE;
+  if (pl->d_in < 1 || pl->d_out < 1 || pl->batch < 1 || pl->n_chains < 1) return DGPRF_E_SHAPE;
+  if (pl->likelihood != DGPRF_LIK_GAUSSIAN && pl->likelihood != DGPRF_LIK_SOFTMAX) return DGPRF_E_ARG;
+  for (int l = 0; l < L; ++l) {
+    if (pl->kind[l] != DGPRF_RBF && pl->kind[l] != DGPRF_ARC) return DGPRF_E_ARG;
+    if (pl->n_rf[l] < 1 || pl->n_gp[l] < 1 || pl->n_gp[l] > DGPRF_MAX_G) return DGPRF_E_SHAPE;
+  }
+  for (int l = L; l < DGPRF_MAX_LAYERS; ++l) {
+    pl->kind[l] = 0;
+    pl->n_rf[l] = 0;
+    pl->n_gp[l] = 0;
+  }
+  // widths: [d_in, n_gp[:-1]] (+ d_in when input_cat)   models/dgp.py:76-79
+  int64_t om = 0, w = 0, lis = 0;
+  for (int l = 0; l < DGPRF_MAX_LAYERS; ++l) {
+    pl->d[l] = pl->P[l] = pl->ns[l] = pl->cpw[l] = 0;
+    pl->omega_off[l] = pl->w_off[l] = pl->lis_off[l] = pl->mean_off[l] = 0;
+    pl->fp_off[l] = pl->dxp_off[l] = 0;
+  }
+  for (int l = 0; l < L; ++l) {
+    pl->d[l] = l == 0 ? pl->d_in : pl->n_gp[l - 1] + (pl->input_cat ? pl->d_in : 0);
+    if (pl->d[l] > DGPRF_MAX_D) return DGPRF_E_SHAPE;
+    pl->P[l] = pl->kind[l] == DGPRF_RBF ? 2 * pl->n_rf[l] : pl->n_rf[l];  // models/dgp.py:103,107
+    pl->omega_off[l] = om;
+    om = align4(om + (int64_t)pl->d[l] * pl->n_rf[l]);
+    pl->w_off[l] = w;
+    w = align4(w + (int64_t)pl->P[l] * pl->n_gp[l]);
+    // step decomposition: <= 16 feature slices of 4 waves x cpw 16-feature chunks
+    const int chunks = (pl->n_rf[l] + 15) / 16;
+    const int cpw = (chunks + 4 * 16 - 1) / (4 * 16);
+    pl->cpw[l] = cpw < 1 ? 1 : cpw;
+    pl->ns[l] = (chunks + 4 * pl->cpw[l] - 1) / (4 * pl->cpw[l]);
+  }
+  pl->omega_total = om;
+  pl->w_total = w;
+  // hyp: log_amp[L] | lik_log_var | pad to 4 | log_inv_ls (sum d) | mean (sum d)
+  lis = align4(L + 1);
+  for (int l = 0; l < L; ++l) {
+    pl->lis_off[l] = lis;
+    lis += pl->d[l];
+  }
+  lis = align4(lis);
+  for (int l = 0; l < L; ++l) {
+    pl->mean_off[l] = lis;
+    lis += pl->d[l];
+  }
+  pl->hyp_total = align4(lis);
+  pl->der_total = DGPRF_MAX_LAYERS + 4;
+  // workspace (per chain)
+  const int B = pl->batch;
+  pl->n_row_tiles = (B + 15) / 16;
+  int64_t ws = 0;
+  for (int l = 0; l < L; ++l) {
+    pl->fp_off[l] = ws;
+    ws = align4(ws + (int64_t)pl->ns[l] * B * pl->n_gp[l]);
+  }
+  for (int l = 1; l < L; ++l) {
+    pl->dxp_off[l] = ws;
+    ws = align4(ws + (int64_t)pl->ns[l] * B * pl->n_gp[l - 1]);
+  }
+  pl->gwp_off = ws;
+  ws = align4(ws + (int64_t)pl->n_row_tiles * pl->w_total);
+  pl->logp_off = ws;
+  ws = align4(ws + B);
+  pl->ws_chain = ws;
+  pl->ws_total = ws * pl->n_chains;
+  pl->pad0 = 0;
+  pl->initialised = 1;
+  return DGPRF_OK;
+}
+
+int dgprf_philox_normal(float* out, int64_t n, uint64_t seed, uint64_t subsequence,
+                        uint32_t purpose, void* stream) {
+  if (n < 0 || (n > 0 && !out) || purpose > 255) return DGPRF_E_ARG;
+  return hip_rc(dgprf::launch_philox_normal(out, n, seed, subsequence, purpose, as_stream(stream)));
+}
+
+int dgprf_omega_build(const dgprf_plan_t* plan, const float* z, const float* hyp, float* omega,
+                      float* der, void* stream) {
+  int rc = check_plan(plan);
+  if (rc) return rc;
+  if (!z || !hyp || !omega || !der) return DGPRF_E_ARG;
+  return hip_rc(dgprf::launch_omega_build(*plan, z, hyp, omega, der, as_stream(stream)));
+}
+
+int dgprf_sghmc_step(const dgprf_plan_t* plan, const dgprf_chain_t* chain,
+                     const dgprf_batch_t* batch, const dgprf_step_t* step, void* stream) {
+  int rc = check_plan(plan);
+  if (!rc) rc = check_chain(chain);
+  if (!rc) rc = check_batch(*plan, batch);
+  if (!rc) rc = check_step(step);
+  if (rc) return rc;
+  dgprf_step_t st = *step;
+  st.grad_only = 0;
+  const StepDev sd = make_step_dev(*plan, *chain, *batch, st.step_offset);
+  const UpdateDev ud = make_update_dev(st);
+  hipError_t e = enqueue_step(*plan, sd, ud, as_stream(stream));
+  if (e == hipSuccess) e = dgprf::launch_advance(chain->step, 1, as_stream(stream));
+  return hip_rc(e);
+}
+
+int dgprf_potential_grad(const dgprf_plan_t* plan, const dgprf_chain_t* chain,
+                         const dgprf_batch_t* batch, float data_size, float* grad_out,
+                         void* stream) {
+  int rc = check_plan(plan);
+  if (!rc) rc = check_chain(chain);
+  if (!rc) rc = check_batch(*plan, batch);
+  if (rc) return rc;
+  if (!grad_out || !(data_size > 0.f)) return DGPRF_E_ARG;
+  StepDev sd = make_step_dev(*plan, *chain, *batch, 0);
+  sd.grad_out = grad_out;
+  dgprf_step_t st;
+  std::memset(&st, 0, sizeof(st));
+  st.data_size = data_size;
+  st.grad_only = 1;
+  return hip_rc(enqueue_step(*plan, sd, make_update_dev(st), as_stream(stream)));
+}
+
+int dgprf_graph_create_sghmc(dgprf_graph_handle* out, const dgprf_plan_t* plan,
+                             const dgprf_chain_t* chain, const dgprf_batch_t* batch,
+                             const dgprf_step_t* step, int32_t steps_per_graph) {
+  if (!out) return DGPRF_E_ARG;
+  *out = nullptr;
+  int rc = check_plan(plan);
+  if (!rc) rc = check_chain(chain);
+  if (!rc) rc = check_batch(*plan, batch);
+  if (!rc) rc = check_step(step);
+  if (rc) return rc;
+  if (steps_per_graph < 1 || step->xi || step->xi_resample) return DGPRF_E_ARG;
+  hipStream_t cs;
+  if (hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess) return DGPRF_E_HIP;
+  hipError_t e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
+  dgprf_step_t st = *step;
+  st.grad_only = 0;
+  const UpdateDev ud = make_update_dev(st);
+  for (int k = 0; k < steps_per_graph && e == hipSuccess; ++k) {
+    const StepDev sd = make_step_dev(*plan, *chain, *batch, st.step_offset + k);
+    e = enqueue_step(*plan, sd, ud, cs);
+  }
+  if (e == hipSuccess) e = dgprf::launch_advance(chain->step, steps_per_graph, cs);
+  hipGraph_t g = nullptr;
+  const hipError_t e2 = hipStreamEndCapture(cs, &g);
+  if (e == hipSuccess) e = e2;
+  hipGraphExec_t ex = nullptr;
+  if (e == hipSuccess) e = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+  (void)hipStreamDestroy(cs);
+  if (e != hipSuccess) {
+    if (g) (void)hipGraphDestroy(g);
+    return DGPRF_E_HIP;
+  }
+  dgprf_graph* h = new (std::nothrow) dgprf_graph;
+  if (!h) {
+    (void)hipGraphExecDestroy(ex);
+    (void)hipGraphDestroy(g);
+    return DGPRF_E_HIP;
+  }
+  h->graph = g;
+  h->exec = ex;
+  *out = h;
+  return DGPRF_OK;
+}
+
+int dgprf_graph_launch(dgprf_graph_handle graph, void* stream) {
+  if (!graph) return DGPRF_E_ARG;
+  return hip_rc(hipGraphLaunch(graph->exec, as_stream(stream)));
+}
+
+int dgprf_graph_destroy(dgprf_graph_handle graph) {
+  if (!graph) return DGPRF_OK;
+  hipError_t e = hipGraphExecDestroy(graph->exec);
+  const hipError_t e2 = hipGraphDestroy(graph->graph);
+  delete graph;
+  return hip_rc(e != hipSuccess ? e : e2);
+}
+
+int dgprf_profile_step(const dgprf_plan_t* plan, const dgprf_chain_t* chain,
+                       const dgprf_batch_t* batch, const dgprf_step_t* step, int32_t reps,
+                       float* ms_out, void* stream) {
+  int rc = check_plan(plan);
+  if (!rc) rc = check_chain(chain);
+  if (!rc) rc = check_batch(*plan, batch);
+  if (!rc) rc = check_step(step);
+  if (rc) return rc;
+  if (!ms_out || reps < 1) return DGPRF_E_ARG;
+  const hipStream_t s = as_stream(stream);
+  dgprf_step_t st = *step;
+  st.grad_only = 0;
+  const StepDev sd = make_step_dev(*plan, *chain, *batch, st.step_offset);
+  const UpdateDev ud = make_update_dev(st);
+  hipError_t e = enqueue_step(*plan, sd, ud, s);
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (e == hipSuccess) e = hipEventCreate(&e0);
+  if (e == hipSuccess) e = hipEventCreate(&e1);
+  const int L = plan->n_layers;
+  for (int k = 0; k < 2 * L + 1 && e == hipSuccess; ++k) {
+    e = hipEventRecord(e0, s);
+    for (int r = 0; r < reps && e == hipSuccess; ++r) {
+      if (k < L) e = dgprf::launch_step_fwd(*plan, sd, k, s);
+      else if (k < 2 * L) e = dgprf::launch_step_bwd(*plan, sd, k - L, s);
+      else e = dgprf::launch_step_update(*plan, sd, ud, nullptr, s);
+    }
+    if (e == hipSuccess) e = hipEventRecord(e1, s);
+    if (e == hipSuccess) e = hipEventSynchronize(e1);
+    float ms = 0.f;
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+    ms_out[k] = ms / (float)reps;
+  }
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  return hip_rc(e);
+}
+
+int dgprf_forward(const dgprf_plan_t* plan, const float* theta, const float* omega,
+                  const float* der, const float* X, const float* Y, int32_t y_cols, int64_t n,
+                  float* const* f_out, float* logp, float* se, float* lse_m, float* lse_s,
+                  float* se_sum, void* stream) {
+  int rc = check_plan(plan);
+  if (rc) return rc;
+  if (!theta || !omega || !der || n < 0 || (n > 0 && !X)) return DGPRF_E_ARG;
+  const bool lik = logp || se || lse_m;
+  if (lik && (!Y || y_cols < 1)) return DGPRF_E_ARG;
+  if ((lse_m == nullptr) != (lse_s == nullptr)) return DGPRF_E_ARG;
+  if (se && plan->likelihood != DGPRF_LIK_GAUSSIAN) return DGPRF_E_ARG;
+  if (lik && plan->likelihood == DGPRF_LIK_GAUSSIAN && y_cols < plan->n_gp[plan->n_layers - 1])
+    return DGPRF_E_SHAPE;
+  return hip_rc(dgprf::launch_forward_rows(*plan, theta, omega, der, X, Y, y_cols, n, f_out, logp,
+                                           se, lse_m, lse_s, se_sum, as_stream(stream)));
+}
+
+int dgprf_lse_finalize(const float* lse_m, const float* lse_s, const float* se_sum, int32_t parts,
+                       int64_t n, double s_total, float log_y_std, float y_std, float* lse_out,
+                       double* out, void* stream) {
+  if (!lse_m || !lse_s || !out || parts < 1 || n < 1 || !(s_total > 0.0)) return DGPRF_E_ARG;
+  return hip_rc(dgprf::launch_lse_finalize(lse_m, lse_s, se_sum, parts, n, s_total, log_y_std,
+                                           y_std, lse_out, out, as_stream(stream)));
+}
+
+int dgprf_rf_omega(int32_t kind, int32_t d, int32_t R, const float* z, const float* log_inv_ls,
+                   const float* mean, const float* log_amp, float* omega, float* c, void* stream) {
+  if ((kind != DGPRF_RBF && kind != DGPRF_ARC) || d < 1 || R < 1) return DGPRF_E_ARG;
+  if (!z || !log_inv_ls || !mean || !log_amp || !omega || !c) return DGPRF_E_ARG;
+  return hip_rc(dgprf::launch_rf_omega(kind, d, R, z, log_inv_ls, mean, log_amp, omega, c,
+                                       as_stream(stream)));
+}
+
+int dgprf_rf_features(int32_t kind, const float* X, int64_t n, int32_t d, const float* omega,
+                      int32_t R, const float* c, float* phi, void* stream) {
+  if ((kind != DGPRF_RBF && kind != DGPRF_ARC) || n < 0 || d < 1 || R < 1) return DGPRF_E_ARG;
+  if (!omega || !c || (n > 0 && (!X || !phi))) return DGPRF_E_ARG;
+  return hip_rc(dgprf::launch_rf_features(kind, X, n, d, omega, R, c, phi, as_stream(stream)));
+}
+
+int dgprf_gp_matmul(const float* phi, int64_t n, int32_t P, const float* W, int32_t g, float* F,
+                    void* stream) {
+  if (n < 0 || P < 1 || g < 1 || !W || (n > 0 && (!phi || !F))) return DGPRF_E_ARG;
+  return hip_rc(dgprf::launch_gp_matmul(phi, n, P, W, g, F, as_stream(stream)));
+}
+
+int dgprf_prior_w(const dgprf_plan_t* plan, const float* theta, float* out, void* stream) {
+  int rc = check_plan(plan);
+  if (rc) return rc;
+  if (!theta || !out) return DGPRF_E_ARG;
+  return hip_rc(dgprf::launch_prior_w(*plan, theta, out, as_stream(stream)));
+}
+
+int dgprf_sghmc_update(const dgprf_plan_t* plan, float* theta, float* mom, const float* grad,
+                       const float* mass, const int64_t* step_ctr, uint64_t seed,
+                       const dgprf_step_t* step, void* stream) {
+  int rc = check_plan(plan);
+  if (!rc) rc = check_step(step);
+  if (rc) return rc;
+  if (!theta || !mom || !grad || !mass || !step_ctr) return DGPRF_E_ARG;
+  StepDev sd;
+  std::memset(&sd, 0, sizeof(sd));
+  sd.theta = theta;
+  sd.mom = mom;
+  sd.mass = mass;
+  sd.step = step_ctr;
+  sd.seed = seed;
+  sd.step_offset = step->step_offset;
+  dgprf_step_t st = *step;
+  st.grad_only = 0;
+  return hip_rc(dgprf::launch_step_update(*plan, sd, make_update_dev(st), grad, as_stream(stream)));
+}
+
+int dgprf_welford_update(const dgprf_plan_t* plan, const float* grad, float* mean, float* m2,
+                         int32_t k, void* stream) {
+  int rc = check_plan(plan);
+  if (rc) return rc;
+  if (!grad || !mean || !m2 || k < 1) return DGPRF_E_ARG;
+  return hip_rc(dgprf::launch_welford(*plan, grad, mean, m2, k, as_stream(stream)));
+}
+
+int dgprf_mass_estimate(const dgprf_plan_t* plan, const float* mean, const float* m2,
+                        int32_t k_batches, int32_t centered, float* mass_est, void* stream) {
+  int rc = check_plan(plan);
+  if (rc) return rc;
+  if (!mean || !m2 || !mass_est || k_batches < 1 || (centered && k_batches < 2)) return DGPRF_E_ARG;
+  return hip_rc(
+      dgprf::launch_mass_estimate(*plan, mean, m2, k_batches, centered, mass_est, as_stream(stream)));
+}
+
+}  // extern "C"

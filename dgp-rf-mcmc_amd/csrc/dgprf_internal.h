@@ -1,0 +1,66 @@
+// dgprf_internal.h — launcher declarations shared by the .hip translation units of libdgprf.so.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "dgprf_device.h"
+
+// Everything a step kernel needs besides the plan (passed by value as a kernel argument).
+struct StepDev {
+  float* theta;
+  float* mom;
+  const float* omega;
+  const float* der;
+  const float* mass;
+  float* ws;
+  const int64_t* step;
+  float* grad_out;  // grad_only mode: [C][w_total]
+  uint64_t seed;
+  BatchDev bd;
+  int32_t step_offset;
+};
+
+struct UpdateDev {
+  float lr, beta, temperature, data_size;
+  int32_t resample, schedule, grad_only, resample_head;
+  int64_t start_step, cycle_length;
+  const float* xi;
+  const float* xi_resample;
+};
+
+namespace dgprf {
+// Dynamic LDS above 64 KiB must be opted into per kernel.
+inline void set_lds_limit(const void* fn, size_t bytes) {
+  if (bytes > 65536) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
+hipError_t launch_step_fwd(const dgprf_plan_t& pl, const StepDev& sd, int layer, hipStream_t s);
+hipError_t launch_step_bwd(const dgprf_plan_t& pl, const StepDev& sd, int layer, hipStream_t s);
+hipError_t launch_step_update(const dgprf_plan_t& pl, const StepDev& sd, const UpdateDev& ud,
+                              const float* grad_in, hipStream_t s);
+hipError_t launch_advance(int64_t* step, int64_t by, hipStream_t s);
+
+hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const float* omega,
+                               const float* der, const float* X, const float* Y, int y_cols,
+                               int64_t n, float* const* f_out, float* logp, float* se,
+                               float* lse_m, float* lse_s, float* se_sum, hipStream_t s);
+hipError_t launch_lse_finalize(const float* lse_m, const float* lse_s, const float* se_sum,
+                               int parts, int64_t n, double s_total, float log_y_std, float y_std,
+                               float* lse_out, double* out, hipStream_t s);
+hipError_t launch_rf_features(int kind, const float* X, int64_t n, int d, const float* omega,
+                              int R, const float* c, float* phi, hipStream_t s);
+hipError_t launch_gp_matmul(const float* phi, int64_t n, int P, const float* W, int g, float* F,
+                            hipStream_t s);
+hipError_t launch_prior_w(const dgprf_plan_t& pl, const float* theta, float* out, hipStream_t s);
+
+hipError_t launch_philox_normal(float* out, int64_t n, uint64_t seed, uint64_t sub,
+                                uint32_t purpose, hipStream_t s);
+hipError_t launch_omega_build(const dgprf_plan_t& pl, const float* z, const float* hyp,
+                              float* omega, float* der, hipStream_t s);
+hipError_t launch_rf_omega(int kind, int d, int R, const float* z, const float* lis,
+                           const float* mean, const float* log_amp, float* omega, float* c,
+                           hipStream_t s);
+hipError_t launch_welford(const dgprf_plan_t& pl, const float* grad, float* mean, float* m2, int k,
+                          hipStream_t s);
+hipError_t launch_mass_estimate(const dgprf_plan_t& pl, const float* mean, const float* m2, int K,
+                                int centered, float* mass_est, hipStream_t s);
+}  // namespace dgprf

@@ -1,0 +1,384 @@
+// predict_kernels.hip — forward / predictive scoring of posterior samples on gfx950.
+//
+// k_forward_rows replaces, for one posterior sample theta_s (or C chains at once):
+//   BNN_from_list(_input_cat).__call__      utils.py:10-16, 32-44
+//   RegressionDGP.eval_log_likelihood_and_se models/regression_model.py:33-50
+//   ClassificationDGP.eval_log_likelihood    models/classification_model.py:49-60
+//   feed_forward_all_layers                  models/regression_model.py:24-31
+// and fuses the driver's posterior-predictive log-sum-exp over samples
+// (experiments/utils_training.py:79-85) as an online (max, sum) accumulator per test point.
+//
+// Geometry: one workgroup = one 16-row tile walking ALL layers; its 4 waves split each layer's RF
+// features (16-feature chunks on v_mfma_f32_16x16x4_f32) and sum their F partials in LDS, so the
+// layer outputs never leave LDS and no cross-workgroup reduction exists.
+#include "dgprf_internal.h"
+
+namespace {
+
+constexpr int NW = DGPRF_WAVES;
+constexpr int TR = DGPRF_TILE_ROWS;
+constexpr float LOG_2PI = 1.8378770664093453f;
+
+__host__ __device__ __forceinline__ int round4(int x) { return (x + 3) & ~3; }
+
+struct FwdLds {
+  int xst, ftst, red_off, ft_off, total;
+};
+
+__host__ __device__ inline FwdLds fwd_lds(const dgprf_plan_t& pl) {
+  int dmax = 4, gmax = 1;
+  for (int l = 0; l < pl.n_layers; ++l) {
+    dmax = pl.d[l] > dmax ? pl.d[l] : dmax;
+    gmax = pl.n_gp[l] > gmax ? pl.n_gp[l] : gmax;
+  }
+  FwdLds L;
+  L.xst = round4(dmax) + 1;
+  L.ftst = round4(gmax) + 1;
+  L.red_off = round4(TR * L.xst);
+  L.ft_off = L.red_off + NW * TR * 64;
+  L.total = L.ft_off + round4(TR * L.ftst);
+  return L;
+}
+
+struct FOut {
+  float* p[DGPRF_MAX_LAYERS];
+};
+
+// One workgroup = one 16-row tile; its 4 waves split each layer's RF features (16-feature chunks
+// w, w+4, ...) and the per-wave F partials are summed in LDS in wave order.
+template <bool SMALLD>
+__global__ __launch_bounds__(256) void k_forward_rows(
+    const dgprf_plan_t pl, const float* __restrict__ theta, const float* __restrict__ omega,
+    const float* __restrict__ der, const float* __restrict__ X, const float* __restrict__ Y,
+    const int y_cols, const int64_t n, const FOut fo, float* __restrict__ logp_out,
+    float* __restrict__ se_out, float* __restrict__ lse_m, float* __restrict__ lse_s,
+    float* __restrict__ se_sum) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const FwdLds LD = fwd_lds(pl);
+  const int chain = blockIdx.y;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, lr = lane & 15, lq = lane >> 4;
+  const int64_t row0 = (int64_t)blockIdx.x * TR;
+  float* xs = smem;
+  float* red = smem + LD.red_off;
+  float* ft = smem + LD.ft_off;
+  const float* Wc = theta + (int64_t)chain * pl.w_total;
+  const int L = pl.n_layers;
+
+  for (int layer = 0; layer < L; ++layer) {
+    const int d = pl.d[layer], dpad = round4(d);
+    const int R = pl.n_rf[layer], g = pl.n_gp[layer];
+    const int gp = layer > 0 ? pl.n_gp[layer - 1] : 0;
+    for (int e = threadIdx.x; e < TR * dpad; e += blockDim.x) {
+      const int r = e / dpad, k = e - r * dpad;
+      const int64_t b = row0 + r;
+      float v = 0.f;
+      if (b < n && k < d) v = (k < gp) ? ft[r * LD.ftst + k] : X[b * pl.d_in + (k - gp)];
+      xs[r * LD.xst + k] = v;
+    }
+    __syncthreads();
+
+    const bool rbf = pl.kind[layer] == DGPRF_RBF;
+    const float* __restrict__ om = omega + pl.omega_off[layer];
+    const float* __restrict__ W = Wc + pl.w_off[layer];
+    const float cl = der[layer];
+    const int NOT = (g + 15) >> 4;
+    float xf[8];
+    if (SMALLD) {
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) xf[ks] = (4 * ks < d) ? xs[lr * LD.xst + 4 * ks + lq] : 0.f;
+    }
+    f4 acc[4] = {f4zero(), f4zero(), f4zero(), f4zero()};
+    for (int f0 = wave * 16; f0 < R; f0 += NW * 16) {
+      const int fa = f0 + lr;
+      const bool fok = fa < R;
+      f4 at = f4zero();
+      if (SMALLD) {
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+          if (4 * ks < d) {
+            const int k = 4 * ks + lq;
+            const float o = (fok && k < d) ? om[(int64_t)k * R + fa] : 0.f;
+            at = mfma16(o, xf[ks], at);
+          }
+        }
+      } else {
+        const int KS = dpad >> 2;
+        for (int ks = 0; ks < KS; ++ks) {
+          const int k = 4 * ks + lq;
+          const float o = (fok && k < d) ? om[(int64_t)k * R + fa] : 0.f;
+          at = mfma16(o, xs[lr * LD.xst + 4 * ks + lq], at);
+        }
+      }
+      float p0[4], p1[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (rbf) {
+          float s, c;
+          rf_sincos(at[r], &s, &c);
+          p0[r] = cl * c;
+          p1[r] = cl * s;
+        } else {
+          p0[r] = cl * fmaxf(at[r], 0.f);
+          p1[r] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int ot = 0; ot < 4; ++ot) {
+        if (ot < NOT) {
+          const int o = ot * 16 + lr;
+          const bool ook = o < g;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int fr = f0 + 4 * lq + r;
+            const bool ok = ook && fr < R;
+            const float wc = ok ? W[(int64_t)fr * g + o] : 0.f;
+            acc[ot] = mfma16(wc, p0[r], acc[ot]);
+            if (rbf) {
+              const float wsn = ok ? W[(int64_t)(R + fr) * g + o] : 0.f;
+              acc[ot] = mfma16(wsn, p1[r], acc[ot]);
+            }
+          }
+        }
+      }
+    }
+    // acc[ot][r] = F partial[row lr][ot*16 + 4lq + r] of this wave's features
+    const int GP = NOT * 16;
+    float* redw = red + wave * TR * GP;
+#pragma unroll
+    for (int ot = 0; ot < 4; ++ot)
+      if (ot < NOT)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) redw[lr * GP + ot * 16 + 4 * lq + r] = acc[ot][r];
+    __syncthreads();
+    float* out = fo.p[layer] ? fo.p[layer] + (int64_t)chain * n * g : nullptr;
+    for (int e = threadIdx.x; e < TR * g; e += blockDim.x) {
+      const int r = e / g, o = e - r * g;
+      float v = red[r * GP + o];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) v += red[w * TR * GP + r * GP + o];
+      ft[r * LD.ftst + o] = v;
+      const int64_t b = row0 + r;
+      if (out && b < n) out[b * g + o] = v;
+    }
+    __syncthreads();
+  }
+
+  // likelihood per row (threads 0..15)
+  const bool want_lik = logp_out || se_out || lse_m;
+  if (want_lik && threadIdx.x < TR) {
+    const int64_t b = row0 + threadIdx.x;
+    if (b < n) {
+      const int g = pl.n_gp[L - 1];
+      const float* f = ft + threadIdx.x * LD.ftst;
+      const float* y = Y + b * y_cols;
+      float lp = 0.f, se = 0.f;
+      if (pl.likelihood == DGPRF_LIK_GAUSSIAN) {
+        const float var = der[DGPRF_MAX_LAYERS];
+        const float logvar = logf(var);
+        for (int o = 0; o < g; ++o) {
+          const float diff = y[o] - f[o];
+          lp += -0.5f * (LOG_2PI + logvar + diff * diff / var);
+          se += diff * diff;
+        }
+        se = se / (float)g;  // reduce_mean over outputs (regression_model.py:46)
+      } else {
+        float mx = -INFINITY;
+        for (int o = 0; o < g; ++o) mx = fmaxf(mx, f[o]);
+        float s = 0.f;
+        for (int o = 0; o < g; ++o) s += expf(f[o] - mx);
+        const int label = min(max((int)y[0], 0), g - 1);
+        lp = f[label] - (mx + logf(s));
+      }
+      const int64_t idx = (int64_t)chain * n + b;
+      if (logp_out) logp_out[idx] = lp;
+      if (se_out) se_out[idx] = se;
+      if (lse_m) {
+        const float m0 = lse_m[idx], s0 = lse_s[idx];
+        const float m1 = fmaxf(m0, lp);
+        lse_s[idx] = s0 * expf(m0 - m1) + expf(lp - m1);
+        lse_m[idx] = m1;
+        if (se_sum) se_sum[idx] += se;
+      }
+    }
+  }
+}
+
+// Combine per-part (chain x rank) accumulators and reduce to the two scalars in a fixed order.
+__global__ __launch_bounds__(1024) void k_lse_finalize(const float* __restrict__ lse_m,
+                                                       const float* __restrict__ lse_s,
+                                                       const float* __restrict__ se_sum,
+                                                       const int parts, const int64_t n,
+                                                       const double s_total, const float log_y_std,
+                                                       const float y_std, float* lse_out,
+                                                       double* out) {
+  __shared__ double r0[1024], r1[1024];
+  double a0 = 0.0, a1 = 0.0;
+  const double log_s = log(s_total);
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+    float m = -INFINITY;
+    for (int p = 0; p < parts; ++p) m = fmaxf(m, lse_m[(int64_t)p * n + i]);
+    float s = 0.f, e = 0.f;
+    for (int p = 0; p < parts; ++p) {
+      s += lse_s[(int64_t)p * n + i] * expf(lse_m[(int64_t)p * n + i] - m);
+      if (se_sum) e += se_sum[(int64_t)p * n + i];
+    }
+    const float lse = m + logf(s);
+    if (lse_out) lse_out[i] = lse;
+    a0 += (double)lse - log_s;
+    a1 += (double)e;
+  }
+  r0[threadIdx.x] = a0;
+  r1[threadIdx.x] = a1;
+  __syncthreads();
+  for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      r0[threadIdx.x] += r0[threadIdx.x + w];
+      r1[threadIdx.x] += r1[threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    out[0] = r0[0] / (double)n - (double)log_y_std;
+    out[1] = sqrt(r1[0] / (s_total * (double)n)) * (double)y_std;
+  }
+}
+
+// Phi = c [cos(X Omega) | sin(X Omega)]  or  c relu(X Omega)  (layers/rf_layers.py:42-44,88-90)
+__global__ __launch_bounds__(256) void k_rf_features(const int kind, const float* __restrict__ X,
+                                                     const int64_t n, const int d,
+                                                     const float* __restrict__ om, const int R,
+                                                     const float* __restrict__ cptr,
+                                                     float* __restrict__ phi) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, lr = lane & 15, lq = lane >> 4;
+  const int64_t row0 = (int64_t)blockIdx.x * TR;
+  const int f0 = (blockIdx.y * NW + wave) * 16;
+  if (f0 >= R) return;
+  const int P = kind == DGPRF_RBF ? 2 * R : R;
+  const float cl = *cptr;
+  const int fa = f0 + lr;
+  const int64_t bx = row0 + lr;
+  f4 at = f4zero();
+  for (int k0 = 0; k0 < d; k0 += 4) {
+    const int k = k0 + lq;
+    const float o = (fa < R && k < d) ? om[(int64_t)k * R + fa] : 0.f;
+    const float x = (bx < n && k < d) ? X[bx * d + k] : 0.f;
+    at = mfma16(o, x, at);
+  }
+  if (bx >= n) return;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int f = f0 + 4 * lq + r;
+    if (f < R) {
+      if (kind == DGPRF_RBF) {
+        float s, c;
+        rf_sincos(at[r], &s, &c);
+        phi[bx * P + f] = cl * c;
+        phi[bx * P + R + f] = cl * s;
+      } else {
+        phi[bx * P + f] = cl * fmaxf(at[r], 0.f);
+      }
+    }
+  }
+}
+
+// F = Phi W (layers/GP_weight_layers.py:13); one thread per output element.
+__global__ void k_gp_matmul(const float* __restrict__ phi, const int64_t n, const int P,
+                            const float* __restrict__ W, const int g, float* __restrict__ F) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * g) return;
+  const int64_t b = i / g;
+  const int o = (int)(i - b * g);
+  float acc = 0.f;
+  for (int k = 0; k < P; ++k) acc = fmaf(phi[b * P + k], W[(int64_t)k * g + o], acc);
+  F[i] = acc;
+}
+
+// sum_l sum log N(W_l; 0, 1) per chain (models/dgp.py:129-136), fixed-order tree reduction.
+__global__ __launch_bounds__(256) void k_prior_w(const dgprf_plan_t pl,
+                                                 const float* __restrict__ theta, float* out) {
+  __shared__ float red[256];
+  const int chain = blockIdx.x;
+  const float* th = theta + (int64_t)chain * pl.w_total;
+  float total = 0.f;
+  for (int l = 0; l < pl.n_layers; ++l) {
+    const int64_t cnt = (int64_t)pl.P[l] * pl.n_gp[l];
+    float a = 0.f;
+    for (int64_t i = threadIdx.x; i < cnt; i += blockDim.x) {
+      const float w = th[pl.w_off[l] + i];
+      a += -0.5f * (LOG_2PI + 0.f + w * w);
+    }
+    red[threadIdx.x] = a;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+      if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+      __syncthreads();
+    }
+    total += red[0];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[chain] = total;
+}
+
+}  // namespace
+
+namespace dgprf {
+
+hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const float* omega,
+                               const float* der, const float* X, const float* Y, int y_cols,
+                               int64_t n, float* const* f_out, float* logp, float* se,
+                               float* lse_m, float* lse_s, float* se_sum, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const FwdLds LD = fwd_lds(pl);
+  FOut fo;
+  for (int l = 0; l < DGPRF_MAX_LAYERS; ++l) fo.p[l] = (f_out && l < pl.n_layers) ? f_out[l] : nullptr;
+  bool smalld = true;
+  for (int l = 0; l < pl.n_layers; ++l) smalld = smalld && pl.d[l] <= 32;
+  dim3 grid((unsigned)((n + TR - 1) / TR), pl.n_chains);
+  const size_t lds = (size_t)LD.total * sizeof(float);
+  if (smalld) {
+    set_lds_limit((const void*)k_forward_rows<true>, lds);
+    hipLaunchKernelGGL(k_forward_rows<true>, grid, dim3(256), lds, s, pl, theta, omega, der, X, Y,
+                       y_cols, n, fo, logp, se, lse_m, lse_s, se_sum);
+  } else {
+    set_lds_limit((const void*)k_forward_rows<false>, lds);
+    hipLaunchKernelGGL(k_forward_rows<false>, grid, dim3(256), lds, s, pl, theta, omega, der, X, Y,
+                       y_cols, n, fo, logp, se, lse_m, lse_s, se_sum);
+  }
+  return hipGetLastError();
+}
+
+size_t forward_rows_lds_bytes(const dgprf_plan_t& pl) {
+  return (size_t)fwd_lds(pl).total * sizeof(float);
+}
+
+hipError_t launch_lse_finalize(const float* lse_m, const float* lse_s, const float* se_sum,
+                               int parts, int64_t n, double s_total, float log_y_std, float y_std,
+                               float* lse_out, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_lse_finalize, dim3(1), dim3(1024), 0, s, lse_m, lse_s, se_sum, parts, n,
+                     s_total, log_y_std, y_std, lse_out, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_rf_features(int kind, const float* X, int64_t n, int d, const float* omega, int R,
+                              const float* c, float* phi, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  dim3 grid((unsigned)((n + TR - 1) / TR), (unsigned)((R + NW * 16 - 1) / (NW * 16)));
+  hipLaunchKernelGGL(k_rf_features, grid, dim3(256), 0, s, kind, X, n, d, omega, R, c, phi);
+  return hipGetLastError();
+}
+
+hipError_t launch_gp_matmul(const float* phi, int64_t n, int P, const float* W, int g, float* F,
+                            hipStream_t s) {
+  const int64_t tot = n * g;
+  if (tot <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_gp_matmul, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, phi, n, P,
+                     W, g, F);
+  return hipGetLastError();
+}
+
+hipError_t launch_prior_w(const dgprf_plan_t& pl, const float* theta, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_prior_w, dim3(pl.n_chains), dim3(256), 0, s, pl, theta, out);
+  return hipGetLastError();
+}
+
+}  // namespace dgprf

@@ -1,0 +1,42 @@
+"""Chain-parallel multi-GPU plumbing: one process per GPU, torch.distributed (RCCL) only at
+prediction time.  Chains are independent, so the sampling phase has no
+collective; the predictive accumulators are all-gathered once."""
+import os
+
+import torch
+import torch.distributed as dist
+
+_M64 = (1 << 64) - 1
+
+
+def world():
+    """(rank, world_size, local_rank) from torch.distributed or the launcher env."""
+    if dist.is_available() and dist.is_initialized():
+        r, w = dist.get_rank(), dist.get_world_size()
+    else:
+        r, w = int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1))
+    return r, w, int(os.environ.get("LOCAL_RANK", r))
+
+
+def rank_seed(seed, rank):
+    """Independent Philox key per rank (splitmix64 of seed and rank)."""
+    z = (int(seed) + 0x9E3779B97F4A7C15 * (int(rank) + 1)) & _M64
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & _M64
+    return z ^ (z >> 31)
+
+
+def gather_accumulators(m, s, e, S_local, group=None):
+    """All-gather per-rank LSE accumulators [C, n] -> [W*C, n] in rank order, and sum S."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return m, s, e, S_local
+    W = dist.get_world_size(group)
+
+    def ag(t):
+        parts = [torch.empty_like(t) for _ in range(W)]
+        dist.all_gather(parts, t.contiguous(), group=group)
+        return torch.cat(parts, dim=0)
+
+    S = torch.tensor([float(S_local)], dtype=torch.float64, device=m.device)
+    dist.all_reduce(S, group=group)
+    return ag(m), ag(s), (ag(e) if e is not None else None), float(S.item())

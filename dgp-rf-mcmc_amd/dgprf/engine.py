@@ -1,0 +1,413 @@
+"""Device-resident chain engine: packed HBM state + the libdgprf.so calls of the hot path.
+
+One Engine holds the state the reference spreads over tf.Variables and their ad-hoc attributes
+(models/dgp.py:66-68, 208-216, 235-296):
+  theta [C, w_total]   every W_l of every chain, packed (GPLayer.W views into it)
+  mom   [C, w_total]   SGHMC momenta (`param.moments`)
+  mass  [C, L]         preconditioner M per W_l (`param.M`)
+  z, omega [omega_total], hyp [hyp_total], der [der_total]   RF frequencies / kernel hyper-params
+  step  int64[1]       device step counter (Philox counter, minibatch position, schedule)
+Workspaces are sized per minibatch size B and cached.  Everything runs on torch's current HIP
+stream; torch only provides memory, streams and collectives.
+"""
+import ctypes
+import math
+
+import torch
+
+from . import _native as N
+
+_F32 = torch.float32
+
+
+def device():
+    """The HIP device the engine runs on.  There is no CPU fallback."""
+    if not torch.cuda.is_available():
+        raise RuntimeError(
+            "dgprf requires an AMD Instinct (gfx950) HIP device; none is visible. "
+            "The DGP-RF hot path has no CPU fallback.")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def as_device(x, dev, dtype=_F32):
+    """Host array / tensor -> contiguous fp32 device tensor (no copy if already there)."""
+    if not torch.is_tensor(x):
+        x = torch.as_tensor(x)
+    return x.to(device=dev, dtype=dtype).contiguous()
+
+
+# ------------------------------------------------------------------ global Philox stream state
+class _RNG:
+    """Replacement of TF's global generator: key = seed, one fresh subsequence per draw."""
+    seed = 0x5EED_D6F5
+    sub = 0
+
+
+def set_seed(seed):
+    _RNG.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    _RNG.sub = 0
+
+
+def next_subsequence():
+    s = _RNG.sub
+    _RNG.sub += 1
+    return s
+
+
+def normal(shape, purpose, dev=None, out=None):
+    """N(0,1) tensor drawn on the device by dgprf_philox_normal."""
+    dev = dev or device()
+    if out is None:
+        out = torch.empty(shape, dtype=_F32, device=dev)
+    N.call("dgprf_philox_normal", ptr(out), out.numel(), _RNG.seed, next_subsequence(),
+           int(purpose), stream())
+    return out
+
+
+# ------------------------------------------------------------------ spec
+class ModelSpec:
+    """Static shape of a DGP_RF (the constructor arguments of models/dgp.py:9-52)."""
+
+    def __init__(self, d_in, d_out, kinds, n_rf, n_gp, input_cat=False, likelihood=N.LIK_GAUSSIAN):
+        self.d_in, self.d_out = int(d_in), int(d_out)
+        self.kinds = [int(k) for k in kinds]
+        self.n_rf = [int(r) for r in n_rf]
+        self.n_gp = [int(g) for g in n_gp]
+        self.input_cat = bool(input_cat)
+        self.likelihood = int(likelihood)
+        self.L = len(self.kinds)
+
+    def plan(self, batch=1, n_chains=1):
+        return N.make_plan(self.d_in, self.d_out, self.kinds, self.n_rf, self.n_gp,
+                           self.input_cat, self.likelihood, batch, n_chains)
+
+
+class Engine:
+    def __init__(self, spec, n_chains=1, dev=None, seed=None):
+        self.spec = spec
+        self.C = int(n_chains)
+        self.dev = dev or device()
+        self.layout = spec.plan(1, self.C)
+        pl = self.layout
+        self.L = spec.L
+        f = lambda n: torch.zeros(int(n), dtype=_F32, device=self.dev)
+        self.theta = torch.zeros(self.C, pl.w_total, dtype=_F32, device=self.dev)
+        self.mom = torch.zeros(self.C, pl.w_total, dtype=_F32, device=self.dev)
+        self.mass = torch.ones(self.C, self.L, dtype=_F32, device=self.dev)
+        self.z = f(max(pl.omega_total, 1))
+        self.omega = f(max(pl.omega_total, 1))
+        self.hyp = f(pl.hyp_total)
+        self.der = f(pl.der_total)
+        self.step_ctr = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        self.seed = _RNG.seed if seed is None else int(seed)
+        self.lik_log_var_source = None  # callable -> device scalar tensor (Gaussian likelihood)
+        self._ws = {}
+        self._graphs = {}
+        self.moments_ready = False
+
+    # ---------------------------------------------------------------- views
+    def W_view(self, l, chain=0):
+        pl = self.layout
+        o, P, g = pl.w_off[l], pl.P[l], pl.n_gp[l]
+        return self.theta[chain, o:o + P * g].view(P, g)
+
+    def mom_view(self, l, chain=0):
+        pl = self.layout
+        o, P, g = pl.w_off[l], pl.P[l], pl.n_gp[l]
+        return self.mom[chain, o:o + P * g].view(P, g)
+
+    def z_view(self, l):
+        pl = self.layout
+        o, d, R = pl.omega_off[l], pl.d[l], pl.n_rf[l]
+        return self.z[o:o + d * R].view(d, R)
+
+    def omega_view(self, l):
+        pl = self.layout
+        o, d, R = pl.omega_off[l], pl.d[l], pl.n_rf[l]
+        return self.omega[o:o + d * R].view(d, R)
+
+    def log_amp_view(self, l):
+        return self.hyp[l:l + 1].view(())
+
+    def lik_log_var_view(self):
+        return self.hyp[self.L:self.L + 1].view(())
+
+    def lis_view(self, l):
+        o = self.layout.lis_off[l]
+        return self.hyp[o:o + self.layout.d[l]]
+
+    def mean_view(self, l):
+        o = self.layout.mean_off[l]
+        return self.hyp[o:o + self.layout.d[l]]
+
+    def c_view(self, l):
+        return self.der[l:l + 1]
+
+    # ---------------------------------------------------------------- init draws
+    def draw_init(self):
+        """z ~ N(0,1), W ~ N(0,1) (layers/rf_layers.py:22, layers/GP_weight_layers.py:9)."""
+        normal(None, N.RNG_Z, out=self.z)
+        normal(None, N.RNG_W, out=self.theta)
+        for l in range(self.L):
+            self.lis_view(l).fill_(-0.5 * math.log(self.layout.d[l]))  # kernels/RBF.py:16-17,40
+
+    def init_moments(self):
+        """param.M = 1, param.moments ~ N(0,1) (models/dgp.py:235-240)."""
+        self.mass.fill_(1.0)
+        normal(None, N.RNG_MOMENTS, out=self.mom)
+        self.moments_ready = True
+
+    # ---------------------------------------------------------------- per-B plans
+    def plan_ws(self, B):
+        B = int(B)
+        if B not in self._ws:
+            pl = self.spec.plan(B, self.C)
+            ws = torch.zeros(max(pl.ws_total, 4), dtype=_F32, device=self.dev)
+            self._ws[B] = (pl, ws)
+        return self._ws[B]
+
+    def chain_struct(self, ws, omega=None):
+        c = N.Chain()
+        c.theta = self.theta.data_ptr()
+        c.mom = self.mom.data_ptr()
+        c.omega = (self.omega if omega is None else omega).data_ptr()
+        c.der = self.der.data_ptr()
+        c.mass = self.mass.data_ptr()
+        c.ws = ws.data_ptr()
+        c.step = self.step_ctr.data_ptr()
+        c.seed = self.seed
+        return c
+
+    @staticmethod
+    def batch_struct(X, Y, mode=N.BATCH_DIRECT, idx=None, iters=0, perm_seed=0):
+        b = N.Batch()
+        b.X, b.Y = X.data_ptr(), Y.data_ptr()
+        b.idx = idx.data_ptr() if idx is not None else None
+        b.n_data = X.shape[0]
+        b.y_cols = Y.shape[1] if Y.dim() == 2 else 1
+        b.mode = mode
+        b.iters_per_epoch = int(iters)
+        b.perm_seed = int(perm_seed)
+        return b
+
+    @staticmethod
+    def step_struct(lr, beta, T, data_size, resample=False, schedule=N.SCHED_CONST,
+                    start_step=0, cycle_length=1, resample_head=False, xi=None, xi_resample=None,
+                    step_offset=0):
+        s = N.Step()
+        s.lr, s.momentum_decay, s.temperature = float(lr), float(beta), float(T)
+        s.data_size = float(data_size)
+        s.resample_moments = int(bool(resample))
+        s.schedule = int(schedule)
+        s.step_offset = int(step_offset)
+        s.grad_only = 0
+        s.start_step, s.cycle_length = int(start_step), int(cycle_length)
+        s.resample_in_cycle_head = int(bool(resample_head))
+        s.xi = xi.data_ptr() if xi is not None else None
+        s.xi_resample = xi_resample.data_ptr() if xi_resample is not None else None
+        return s
+
+    # ---------------------------------------------------------------- hyper-params
+    def build_omega(self, z=None, omega=None):
+        """Omega, c_l and sigma^2 from z / hyp (dgprf_omega_build); z/omega may be overridden
+        (fresh z of layers with random_fixed=False, layers/rf_layers.py:39-41)."""
+        if self.lik_log_var_source is not None:
+            src = self.lik_log_var_source()
+            if src is not None:
+                self.lik_log_var_view().copy_(src.detach().reshape(()))
+        N.call("dgprf_omega_build", ctypes.byref(self.layout),
+               ptr(self.z if z is None else z), ptr(self.hyp),
+               ptr(self.omega if omega is None else omega), ptr(self.der), stream())
+
+    # ---------------------------------------------------------------- hot path
+    def _prep_batch(self, X, Y):
+        X = as_device(X, self.dev)
+        Y = as_device(Y, self.dev)
+        if X.dim() != 2 or X.shape[1] != self.spec.d_in:
+            raise ValueError(f"X must be [B, {self.spec.d_in}], got {tuple(X.shape)}")
+        if Y.dim() == 1:
+            Y = Y[:, None]
+        if Y.shape[0] != X.shape[0]:
+            raise ValueError("X and Y must have the same number of rows")
+        return X, Y
+
+    def _batch(self, X, Y, batch_size, mode, idx, perm_seed):
+        """(plan, ws, Batch struct, keep-alive) for a DIRECT batch (X, Y are the batch) or an
+        INDEXED / EPOCH minibatch of batch_size rows drawn from the dataset (X, Y)."""
+        X, Y = self._prep_batch(X, Y)
+        B = X.shape[0] if mode == N.BATCH_DIRECT else int(batch_size)
+        pl, ws = self.plan_ws(B)
+        if idx is not None:
+            idx = torch.as_tensor(idx).to(device=self.dev, dtype=torch.int32).contiguous()
+        iters = X.shape[0] // B if mode == N.BATCH_EPOCH else 0
+        bt = self.batch_struct(X, Y, mode, idx, iters, perm_seed)
+        return pl, ws, bt, (X, Y, idx)
+
+    def step(self, X, Y, data_size, lr, beta, T, resample=False, xi=None, xi_resample=None,
+             build=True, omega=None, batch_size=None, mode=N.BATCH_DIRECT, idx=None,
+             perm_seed=0):
+        """One sgmcmc_update (default: X, Y are the batch, DGPRF_BATCH_DIRECT)."""
+        pl, ws, bt, keep = self._batch(X, Y, batch_size, mode, idx, perm_seed)
+        if build:
+            self.build_omega()
+        ch = self.chain_struct(ws, omega)
+        xi = None if xi is None else as_device(xi, self.dev)
+        xr = None if xi_resample is None else as_device(xi_resample, self.dev)
+        st = self.step_struct(lr, beta, T, data_size, resample, xi=xi, xi_resample=xr)
+        N.call("dgprf_sghmc_step", ctypes.byref(pl), ctypes.byref(ch), ctypes.byref(bt),
+               ctypes.byref(st), stream())
+
+    def grad(self, X, Y, data_size, build=True, omega=None, batch_size=None,
+             mode=N.BATCH_DIRECT, idx=None, perm_seed=0):
+        """dU/dW for every layer and chain -> [C, w_total] (dgprf_potential_grad)."""
+        pl, ws, bt, keep = self._batch(X, Y, batch_size, mode, idx, perm_seed)
+        if build:
+            self.build_omega()
+        out = torch.empty(self.C, self.layout.w_total, dtype=_F32, device=self.dev)
+        ch = self.chain_struct(ws, omega)
+        N.call("dgprf_potential_grad", ctypes.byref(pl), ctypes.byref(ch), ctypes.byref(bt),
+               float(data_size), ptr(out), stream())
+        return out
+
+    def graph(self, X_all, Y_all, batch_size, data_size, lr, beta, T, steps_per_graph,
+              schedule=N.SCHED_CONST, start_step=0, cycle_length=1, resample_head=False,
+              perm_seed=0):
+        """hipGraph of `steps_per_graph` on-device-minibatched steps (DGPRF_BATCH_EPOCH)."""
+        key = (X_all.data_ptr(), Y_all.data_ptr(), int(batch_size), float(data_size), float(lr),
+               float(beta), float(T), int(steps_per_graph), int(schedule), int(start_step),
+               int(cycle_length), bool(resample_head), int(perm_seed))
+        if key in self._graphs:
+            return self._graphs[key]
+        pl, ws = self.plan_ws(batch_size)
+        iters = X_all.shape[0] // int(batch_size)
+        ch = self.chain_struct(ws)
+        bt = self.batch_struct(X_all, Y_all, N.BATCH_EPOCH, iters=iters, perm_seed=perm_seed)
+        st = self.step_struct(lr, beta, T, data_size, False, schedule, start_step, cycle_length,
+                              resample_head)
+        h = ctypes.c_void_p()
+        N.call("dgprf_graph_create_sghmc", ctypes.byref(h), ctypes.byref(pl), ctypes.byref(ch),
+               ctypes.byref(bt), ctypes.byref(st), int(steps_per_graph))
+        g = _Graph(h, (X_all, Y_all, ws))
+        self._graphs[key] = g
+        return g
+
+    def profile_step(self, X_all, Y_all, batch_size, data_size, lr, beta, T, reps=200,
+                     perm_seed=0):
+        """Average device ms per launch of each step kernel (hipEvents, dgprf_profile_step):
+        {'fwd': [L], 'bwd': [L], 'update': float}."""
+        pl, ws, bt, keep = self._batch(X_all, Y_all, batch_size, N.BATCH_EPOCH, None, perm_seed)
+        ch = self.chain_struct(ws)
+        st = self.step_struct(lr, beta, T, data_size)
+        ms = (ctypes.c_float * (2 * self.L + 1))()
+        N.call("dgprf_profile_step", ctypes.byref(pl), ctypes.byref(ch), ctypes.byref(bt),
+               ctypes.byref(st), int(reps), ctypes.cast(ms, ctypes.c_void_p), stream())
+        v = list(ms)
+        return {"fwd": v[:self.L], "bwd": v[self.L:2 * self.L], "update": v[2 * self.L]}
+
+    # ---------------------------------------------------------------- forward / predictive
+    def forward(self, X, Y=None, f_out=False, logp=False, se=False, lse=None, omega=None,
+                build=True):
+        """dgprf_forward over all rows of X for every chain.
+
+        Returns a dict with the requested outputs ('F' = list of per-layer [C, n, g_l] when
+        f_out='all', or the last layer only when f_out=True; 'logp', 'se' = [C, n]).
+        `lse` = (m, s, se_sum) accumulators [C, n] updated in place.
+        """
+        X = as_device(X, self.dev)
+        n = X.shape[0]
+        if X.dim() != 2 or X.shape[1] != self.spec.d_in:
+            raise ValueError(f"X must be [n, {self.spec.d_in}], got {tuple(X.shape)}")
+        if build:
+            self.build_omega()
+        out = {}
+        fptrs = (ctypes.c_void_p * N.MAX_LAYERS)()
+        if f_out:
+            Fs = []
+            for l in range(self.L):
+                if f_out == "all" or l == self.L - 1:
+                    t = torch.empty(self.C, n, self.layout.n_gp[l], dtype=_F32, device=self.dev)
+                    fptrs[l] = t.data_ptr()
+                    Fs.append(t)
+            out["F"] = Fs
+        y_cols, Yd = 0, None
+        if Y is not None:
+            Yd = as_device(Y, self.dev)
+            if Yd.dim() == 1:
+                Yd = Yd[:, None]
+            y_cols = Yd.shape[1]
+        lp = torch.empty(self.C, n, dtype=_F32, device=self.dev) if logp else None
+        sq = torch.empty(self.C, n, dtype=_F32, device=self.dev) if se else None
+        if lp is not None:
+            out["logp"] = lp
+        if sq is not None:
+            out["se"] = sq
+        m = s = e = None
+        if lse is not None:
+            m, s, e = lse
+        om = self.omega if omega is None else omega
+        N.call("dgprf_forward", ctypes.byref(self.layout), ptr(self.theta), ptr(om),
+               ptr(self.der), ptr(X), ptr(Yd), int(y_cols), int(n), fptrs, ptr(lp), ptr(sq),
+               ptr(m), ptr(s), ptr(e), stream())
+        out["_keep"] = (X, Yd)
+        return out
+
+    def prior_w(self):
+        out = torch.empty(self.C, dtype=_F32, device=self.dev)
+        N.call("dgprf_prior_w", ctypes.byref(self.layout), ptr(self.theta), ptr(out), stream())
+        return out
+
+    # ---------------------------------------------------------------- preconditioner
+    def welford(self, grad, mean, m2, k):
+        N.call("dgprf_welford_update", ctypes.byref(self.layout), ptr(grad), ptr(mean), ptr(m2),
+               int(k), stream())
+
+    def mass_estimate(self, mean, m2, K, centered):
+        out = torch.empty(self.C, self.L, dtype=_F32, device=self.dev)
+        N.call("dgprf_mass_estimate", ctypes.byref(self.layout), ptr(mean), ptr(m2), int(K),
+               int(bool(centered)), ptr(out), stream())
+        return out
+
+    def sghmc_update(self, grad, lr, beta, T, data_size, resample=False, xi=None,
+                     xi_resample=None):
+        """Stand-alone update from a given gradient [C, w_total] (dgprf_sghmc_update)."""
+        st = self.step_struct(lr, beta, T, data_size, resample,
+                              xi=None if xi is None else as_device(xi, self.dev),
+                              xi_resample=None if xi_resample is None else as_device(xi_resample, self.dev))
+        grad = as_device(grad, self.dev)
+        N.call("dgprf_sghmc_update", ctypes.byref(self.layout), ptr(self.theta), ptr(self.mom),
+               ptr(grad), ptr(self.mass), ptr(self.step_ctr), self.seed, ctypes.byref(st),
+               stream())
+
+
+class _Graph:
+    def __init__(self, handle, keep):
+        self.h = handle
+        self._keep = keep
+
+    def launch(self):
+        N.call("dgprf_graph_launch", self.h, stream())
+
+    def __del__(self):
+        try:
+            if self.h:
+                N.lib().dgprf_graph_destroy(self.h)
+        except Exception:
+            pass
+
+
+def lse_finalize(lse_m, lse_s, se_sum, s_total, y_std=1.0, lse_out=False):
+    """Posterior-predictive LL / RMSE from stacked accumulators [parts, n] (dgprf_lse_finalize)."""
+    parts, n = lse_m.shape
+    out = torch.zeros(2, dtype=torch.float64, device=lse_m.device)
+    lo = torch.empty(n, dtype=_F32, device=lse_m.device) if lse_out else None
+    N.call("dgprf_lse_finalize", ptr(lse_m), ptr(lse_s), ptr(se_sum), int(parts), int(n),
+           float(s_total), float(math.log(y_std)), float(y_std), ptr(lo), ptr(out), stream())
+    return out, lo

@@ -1,0 +1,43 @@
+"""Posterior-predictive accumulation over samples, chains and ranks.
+
+Replaces the driver's `log_p.append(...)` + stack + reduce_logsumexp (experiments/utils_training.py:
+63-65, 79-85): each sample's test log-likelihoods are folded into an online (max, sum) per test
+point by the forward kernel itself, so no [S, N_test] matrix is materialised.  Across GPUs the
+per-rank accumulators are all-gathered once (RCCL over xGMI) at finalize time.
+"""
+import math
+
+import torch
+
+from . import engine as E
+from . import distributed as D
+
+
+class PredictiveLSE:
+    def __init__(self, engine, X_test, Y_test):
+        self.eng = engine
+        self.X = E.as_device(X_test, engine.dev)
+        Y = E.as_device(Y_test, engine.dev)
+        self.Y = Y[:, None] if Y.dim() == 1 else Y
+        n = self.X.shape[0]
+        C = engine.C
+        self.m = torch.full((C, n), -math.inf, dtype=torch.float32, device=engine.dev)
+        self.s = torch.zeros((C, n), dtype=torch.float32, device=engine.dev)
+        self.gaussian = engine.spec.likelihood == 0
+        self.e = torch.zeros((C, n), dtype=torch.float32, device=engine.dev) if self.gaussian \
+            else None
+        self.S = 0  # samples folded in (per rank, all chains)
+
+    def add_sample(self, build=True, omega=None):
+        """Score the engine's current theta (one sample per chain) on the test set."""
+        self.eng.forward(self.X, self.Y, lse=(self.m, self.s, self.e), build=build, omega=omega)
+        self.S += self.eng.C
+
+    def finalize(self, y_std=1.0, group=None):
+        """(test log-likelihood, RMSE) over every sample of every chain of every rank."""
+        m, s, e, S = D.gather_accumulators(self.m, self.s, self.e, self.S, group)
+        if e is None:
+            e = torch.zeros_like(s)
+        out, _ = E.lse_finalize(m, s, e, S, y_std)
+        out = out.cpu()
+        return float(out[0]), (float(out[1]) if self.gaussian else None)

@@ -1,0 +1,323 @@
+"""DGP_RF — mirror of the reference's models/dgp.py:8-304 on the MI355X engine.
+
+Same constructor, properties and methods; the state the reference keeps in tf.Variables lives in
+one packed HBM engine (dgprf.Engine) and the layer/kernel objects hold views into it, so
+`model.BNN.layers[1].W`, `model.W_mcmc`, `kernel.log_amplitude`, ... are live device tensors.
+Compute (forward, likelihood, analytic backward, SGHMC/SGLD update, predictive scoring,
+RMSprop preconditioner statistics) runs in libdgprf.so.
+"""
+import numpy as np
+import torch
+
+from dgprf import _native as N
+from dgprf import engine as E
+from dgprf.module import Module, rebind
+from kernels import ARCKernel, RBFKernel
+from layers import ARCLayer, GPLayer, RBFLayer
+from likelihoods import Gaussian, Softmax
+from utils import BNN_from_list, BNN_from_list_input_cat, log_gaussian
+
+
+def _per_layer(v, L, what):
+    """Scalar -> [v]*L, list -> list (models/dgp.py:34-43)."""
+    if np.ndim(v) == 0:
+        out = [int(v)] * L
+    else:
+        out = [int(x) for x in np.asarray(v).reshape(-1)]
+    assert len(out) == L, f"Error in #{what}!"
+    return out
+
+
+class DGP_RF(Module):
+    def __init__(self, d_in, d_out, n_hidden_layers=1, n_rf=20, n_gp=2, likelihood=Softmax(),
+                 kernel_type_list=None, kernel_trainable=True, random_fixed=True, input_cat=False,
+                 set_nonzero_mean=False, name=None):
+        """
+        :param d_in: Input dim
+        :param d_out: Output dim
+        :param n_hidden_layers: Number of hidden layers
+        :param n_rf: Number of random features
+        :param n_gp: Number of latent GPs in each layer
+        :param likelihood: Likelihood class in the last layer
+        :param kernel_type_list: kernel type list, set is_ard default True
+        :param kernel_trainable: fix the trainable variables or not
+        :param random_fixed: z fixed or not when feeding forward
+        :param input_cat: concatenate input to each hidden layer except the final layer
+        """
+        super().__init__(name=name)
+        self.d_in = d_in
+        self.d_out = d_out
+        self.n_hidden_layers = n_hidden_layers
+        self.random_fixed = random_fixed
+        self.input_cat = input_cat
+        self.set_nonzero_mean = set_nonzero_mean
+        self.kernel_trainable = kernel_trainable
+        self.likelihood = likelihood
+        self.n_rf = _per_layer(n_rf, n_hidden_layers, "random feature layers")
+        self.n_gp = _per_layer(n_gp, n_hidden_layers, "hidden GP layers")
+        if kernel_type_list is None:
+            self.kernel_type_list = ['RBF' for _ in range(n_hidden_layers)]
+        else:
+            assert len(kernel_type_list) == n_hidden_layers, "Kernel type list's length does not match!"
+            self.kernel_type_list = kernel_type_list
+        self.kernel_list = self.transform_kernel_list()
+        self.BNN = self.transformed_BNN()
+        self._bind_engine()
+
+    # ------------------------------------------------------------------ construction
+    def transform_kernel_list(self):
+        """models/dgp.py:74-91."""
+        kernel_list = []
+        if not self.input_cat:
+            before_n_rf = [self.d_in] + self.n_gp[:-1]
+        else:
+            before_n_rf = [self.d_in] + [g + self.d_in for g in self.n_gp[:-1]]
+        for i, kernel_type in enumerate(self.kernel_type_list):
+            if kernel_type == 'RBF':
+                kernel = RBFKernel(n_feature=before_n_rf[i], trainable=self.kernel_trainable,
+                                   is_ard=True, length_scale=None)
+            elif kernel_type == 'ARC':
+                kernel = ARCKernel(n_feature=before_n_rf[i], trainable=self.kernel_trainable,
+                                   is_ard=True, length_scale=None)
+            else:
+                raise NotImplementedError
+            kernel_list.append(kernel)
+        return kernel_list
+
+    def transformed_BNN(self):
+        """models/dgp.py:93-115."""
+        bnn = []
+        for l in range(self.n_hidden_layers):
+            kernel_tmp = self.kernel_list[l]
+            if kernel_tmp.kernel_type == "RBF":
+                layer_Omega = RBFLayer(kernel_tmp, self.n_rf[l], random_fixed=self.random_fixed,
+                                       set_nonzero_mean=self.set_nonzero_mean)
+                layer_GP = GPLayer(2 * self.n_rf[l], self.n_gp[l])
+            elif kernel_tmp.kernel_type == "ARC":
+                layer_Omega = ARCLayer(kernel_tmp, self.n_rf[l], random_fixed=self.random_fixed,
+                                       set_nonzero_mean=self.set_nonzero_mean)
+                layer_GP = GPLayer(self.n_rf[l], self.n_gp[l])
+            else:
+                raise NotImplementedError
+            bnn.extend([layer_Omega, layer_GP])
+        if not self.input_cat:
+            return BNN_from_list(bnn)
+        return BNN_from_list_input_cat(bnn)
+
+    def _lik_code(self):
+        if isinstance(self.likelihood, Gaussian):
+            return N.LIK_GAUSSIAN
+        if isinstance(self.likelihood, Softmax):
+            return N.LIK_SOFTMAX
+        raise NotImplementedError  # models/dgp.py:158-159
+
+    def _bind_engine(self):
+        """Pack every layer's state into one Engine and rebind the objects to views of it."""
+        kinds = [N.RBF if k == 'RBF' else N.ARC for k in self.kernel_type_list]
+        spec = E.ModelSpec(self.d_in, self.d_out, kinds, self.n_rf, self.n_gp, self.input_cat,
+                           self._lik_code())
+        eng = E.Engine(spec, n_chains=1)
+        for l in range(self.n_hidden_layers):
+            rf, gp, k = self.BNN.layers[2 * l], self.BNN.layers[2 * l + 1], self.kernel_list[l]
+            gp.W = rebind(gp.W, eng.W_view(l))
+            k.log_amplitude = rebind(k.log_amplitude, eng.log_amp_view(l))
+            k.log_inv_length_scale = rebind(k.log_inv_length_scale, eng.lis_view(l))
+            rf.mean = rebind(rf.mean, eng.mean_view(l).view(-1, 1))
+        self._engine = eng
+        self._rebind_z()
+        if isinstance(self.likelihood, Gaussian):
+            eng.lik_log_var_source = lambda: self.likelihood.lik_log_var
+        self.BNN._model = self
+
+    def _rebind_z(self):
+        eng = self._engine
+        for l in range(self.n_hidden_layers):
+            rf = self.BNN.layers[2 * l]
+            if hasattr(rf, "z") and rf.z.data_ptr() != eng.z_view(l).data_ptr():
+                rf.z = rebind(rf.z, eng.z_view(l))
+                rf.z.trainable = False
+
+    # ------------------------------------------------------------------ properties
+    @property
+    def Likelihood_hyperparams(self):
+        return list(self.likelihood.trainable_variables)
+
+    @property
+    def Omega_hyperparams(self):
+        params = []
+        for l in range(self.n_hidden_layers):
+            params.extend(list(self.BNN.layers[2 * l].trainable_variables))
+        return params
+
+    @property
+    def W_mcmc(self):
+        return [self.BNN.layers[2 * l + 1].W for l in range(self.n_hidden_layers)]
+
+    def assign_W(self, W_value_list):
+        for gp_layer, W_value in zip(self.BNN.gp_layers, W_value_list):
+            gp_layer.assign_W(W_value)
+
+    # ------------------------------------------------------------------ device helpers
+    def _omega_for_call(self):
+        """Build Omega for this call; layers with random_fixed=False get fresh z (rf_layers.py:39-41)."""
+        eng = self._engine
+        fresh = [l for l in range(self.n_hidden_layers) if not self.BNN.layers[2 * l].random_fixed]
+        if not fresh:
+            eng.build_omega()
+            return None
+        z = eng.z.clone()
+        for l in fresh:
+            pl = eng.layout
+            o, n = pl.omega_off[l], pl.d[l] * pl.n_rf[l]
+            E.normal(None, N.RNG_Z, out=z[o:o + n])
+        om = torch.empty_like(eng.omega)
+        eng.build_omega(z=z, omega=om)
+        return om
+
+    def _fused_forward(self, X):
+        om = self._omega_for_call()
+        out = self._engine.forward(X, f_out=True, omega=om, build=False)
+        return out["F"][0][0]
+
+    # ------------------------------------------------------------------ potential
+    def log_likelihood(self, X, Y, allow_gradient_from_W=True):
+        """log p(Y | X, all params) per row [N] (models/dgp.py:118-127)."""
+        om = self._omega_for_call()
+        return self._engine.forward(X, Y, logp=True, omega=om, build=False)["logp"][0]
+
+    def prior_W(self):
+        """log p(W) ~ N(0, I) (models/dgp.py:129-136)."""
+        return self._engine.prior_w()[0]
+
+    def prior_kernel_params(self):
+        """models/dgp.py:138-147."""
+        log_p = 0.
+        for l in range(self.n_hidden_layers):
+            k = self.BNN.layers[2 * l].kernel
+            log_p = log_p + torch.sum(log_gaussian(k.log_amplitude, mean=0., var=1.))
+            log_p = log_p + torch.sum(log_gaussian(k.log_inv_length_scale, mean=0., var=1.))
+        return log_p
+
+    def prior_likelihood_params(self):
+        """models/dgp.py:149-159."""
+        if isinstance(self.likelihood, Softmax):
+            return 0.
+        elif isinstance(self.likelihood, Gaussian):
+            log_p = 0.
+            for var in self.likelihood.trainable_variables:
+                log_p = log_p + torch.sum(log_gaussian(var, mean=0., var=1.))
+            return log_p
+        else:
+            raise NotImplementedError
+
+    def U(self, X_batch, Y_batch, data_size, full_bayesian=False, allow_gradient_from_W=True):
+        """Minibatch potential -(1/B) sum log p(y|x,w) - (1/N) log p(w)  (models/dgp.py:161-182)."""
+        B = float(np.shape(X_batch)[0])
+        N_ = float(data_size)
+        ll = torch.sum(self.log_likelihood(X_batch, Y_batch)) / B
+        if not full_bayesian:
+            prior = self.prior_W() / N_ if allow_gradient_from_W else 0.
+        else:
+            assert allow_gradient_from_W == True, "Full Bayes should allow gradients from W!"  # noqa: E712
+            prior = 0.
+            for param in self.trainable_variables:
+                prior = prior + torch.sum(log_gaussian(param, mean=0., var=1.)) / N_
+        return -(prior + ll)
+
+    # ------------------------------------------------------------------ sampler
+    def _check_moments(self):
+        if not self._engine.moments_ready:
+            raise AssertionError("Trainable Params do not have attr moments!")  # dgp.py:208
+
+    def _attach_sampler_attrs(self):
+        eng = self._engine
+        for l, W in enumerate(self.W_mcmc):
+            W.moments = eng.mom_view(l)
+            W.M = eng.mass[0, l]
+
+    def sgmcmc_update(self, X_batch, Y_batch, data_size, lr=0.01, momentum_decay=0.95,
+                      resample_moments=False, temperature=1., full_bayesian=False):
+        """One SGHMC (SGLD when momentum_decay = 0) step for W (models/dgp.py:184-216):
+        m <- b m - h N dU/dW + sqrt(2(1-b) T M) xi,  W <- W + h m / M,  h = sqrt(lr / N).
+        Runs as one fused forward/backward/update sequence of HIP kernels."""
+        if full_bayesian:
+            raise NotImplementedError(
+                "full_bayesian=True (gradients w.r.t. kernel/likelihood hyper-parameters, "
+                "models/dgp.py:175-181,199-204) is not implemented by the HIP engine yet")
+        self._check_moments()
+        om = self._omega_for_call()
+        self._engine.step(X_batch, Y_batch, data_size, lr, momentum_decay, temperature,
+                          bool(resample_moments), build=False, omega=om)
+
+    def precond_update(self, ds, data_size, K_batches=32, full_bayesian=False,
+                       precond_type='rmsprop', second_moment_centered=False):
+        """Preconditioner M per W_l from K minibatch gradients (models/dgp.py:218-299):
+        Welford mean/M2 on the device, mass = sqrt(mean(E[g^2]) + 1e-7) (or the centred
+        variance), normalised by the smallest mass; momenta rescaled by sqrt(M)."""
+        if full_bayesian:
+            raise NotImplementedError(
+                "full_bayesian=True preconditioning is not implemented by the HIP engine yet")
+        eng = self._engine
+        if not eng.moments_ready:
+            eng.init_moments()
+            self._attach_sampler_attrs()
+        if precond_type == 'identity':
+            return None
+        elif precond_type == 'rmsprop':
+            L = self.n_hidden_layers
+            m_c = [torch.rsqrt(eng.mass[0, l]) * eng.mom_view(l) for l in range(L)]
+            mean = torch.zeros_like(eng.theta)
+            m2 = torch.zeros_like(eng.theta)
+            om = self._omega_for_call()
+            k = 0
+            for X_batch, Y_batch in ds:
+                g = eng.grad(X_batch, Y_batch, data_size, build=False, omega=om)
+                k = k + 1
+                eng.welford(g, mean, m2, k)
+                if k == K_batches:
+                    break
+            assert k == K_batches, \
+                f"Estimating M ends before we use {K_batches} batches, we actually use {k} batches!"
+            mass_est = eng.mass_estimate(mean, m2, K_batches, second_moment_centered)
+            self._mass_estimate = mass_est[0]
+            mass_min = torch.min(mass_est[0])
+            eng.mass.copy_(mass_est / mass_min)
+            for l in range(L):
+                eng.mom_view(l).copy_(torch.sqrt(eng.mass[0, l]) * m_c[l])
+            return None
+        else:
+            raise NotImplementedError
+
+    def set_random_fixed(self, state):
+        for l in range(self.n_hidden_layers):
+            self.BNN.layers[2 * l].set_random_fixed(state)
+        self._rebind_z()
+
+    # ------------------------------------------------------------------ engine-path sampling
+    def run_sgmcmc(self, X_all, Y_all, data_size, n_steps, batch_size=200, lr=0.01,
+                   momentum_decay=0.9, temperature=1., steps_per_graph=50, perm_seed=0,
+                   schedule=None, start_step=0, cycle_length=1, resample_in_cycle_head=False):
+        """Run n_steps sgmcmc_update steps with device-resident data: per-epoch shuffled,
+        drop-remainder minibatches (experiments/utils_dataset.py:38-42) drawn on the device and
+        `steps_per_graph` steps per hipGraph replay.  schedule='cyclical' applies the driver's
+        burn-in + cosine schedule on the device (experiments/utils_training.py:41-61)."""
+        self._check_moments()
+        eng = self._engine
+        if not all(self.BNN.layers[2 * l].random_fixed for l in range(self.n_hidden_layers)):
+            raise NotImplementedError("run_sgmcmc needs random_fixed=True")
+        X_all = E.as_device(X_all, eng.dev)
+        Y_all = E.as_device(Y_all, eng.dev)
+        if Y_all.dim() == 1:
+            Y_all = Y_all[:, None]
+        eng.build_omega()
+        sched = N.SCHED_CYCLICAL if schedule == 'cyclical' else N.SCHED_CONST
+        spg = max(1, min(int(steps_per_graph), int(n_steps)))
+        g = eng.graph(X_all, Y_all, batch_size, data_size, lr, momentum_decay, temperature, spg,
+                      sched, start_step, cycle_length, resample_in_cycle_head, perm_seed)
+        full, rest = divmod(int(n_steps), spg)
+        for _ in range(full):
+            g.launch()
+        if rest:
+            g2 = eng.graph(X_all, Y_all, batch_size, data_size, lr, momentum_decay, temperature,
+                           rest, sched, start_step, cycle_length, resample_in_cycle_head, perm_seed)
+            g2.launch()

@@ -1,0 +1,275 @@
+/*
+ * dgprf.h — C-ABI of the MI355X-native DGP-RF SGHMC/SGLD engine (libdgprf.so).
+ *
+ * The reference (shixinxing/DGP-RF-MCMC) has no FFI: its hot path is TensorFlow-eager Python
+ * (models/dgp.py, layers/rf_layers.py, layers/GP_weight_layers.py, kernels/RBF.py,
+ * kernels/arc_cosine.py, likelihoods/{gaussian,softmax}.py, utils.py).  The Python mirror of that API
+ * (dgp-rf-mcmc_amd/{models,layers,kernels,likelihoods}, utils.py) binds these entry points with
+ * ctypes.  Every entry point below names the reference code it replaces.
+ *
+ * Conventions
+ *  - All tensors are device pointers (HBM), fp32, row-major, exactly the TF layout of the
+ *    reference (models/dgp.py:118-127; layers/rf_layers.py:42-44; layers/GP_weight_layers.py:13).
+ *  - `stream` is a hipStream_t passed as void* (NULL = legacy default stream).  Every call is
+ *    asynchronous w.r.t. the host and enqueues on that stream only.
+ *  - Return value: 0 on success, a negative DGPRF_E* code otherwise (dgprf_error_string()).
+ *    Shape/config errors are detected on the host before anything is enqueued.
+ *  - No torch types cross this boundary.
+ */
+#ifndef DGPRF_H
+#define DGPRF_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DGPRF_ABI_VERSION 1
+
+#define DGPRF_MAX_LAYERS 8
+#define DGPRF_MAX_G 64        /* max latent GPs per layer (n_gp[l]) */
+#define DGPRF_MAX_D 2048      /* max layer input width d_l */
+
+/* kernel types: models/dgp.py:80-90 (kernel_type_list entries 'RBF' / 'ARC') */
+#define DGPRF_RBF 0
+#define DGPRF_ARC 1
+
+/* likelihoods: likelihoods/gaussian.py:6-25, likelihoods/softmax.py:4-22 */
+#define DGPRF_LIK_GAUSSIAN 0
+#define DGPRF_LIK_SOFTMAX 1
+
+/* minibatch source modes (dgprf_batch_t.mode) */
+#define DGPRF_BATCH_DIRECT 0   /* rows 0..B-1 of X/Y are the batch (sgmcmc_update(X_batch, ...)) */
+#define DGPRF_BATCH_INDEXED 1  /* batch row b of chain c is X[idx[c*B + b]] */
+#define DGPRF_BATCH_EPOCH 2    /* per-epoch keyed Feistel permutation of [0,N), drop-remainder */
+
+/* step-size schedules (dgprf_step_t.schedule) */
+#define DGPRF_SCHED_CONST 0    /* lr, temperature, resample as given */
+#define DGPRF_SCHED_CYCLICAL 1 /* experiments/utils_training.py:41-61 + utils.py:49-73 on device */
+
+/* Philox stream purposes (counter word 3, bits 24..31) */
+#define DGPRF_RNG_NOISE 1      /* xi in m += sqrt(2(1-b)TM) xi   (models/dgp.py:212) */
+#define DGPRF_RNG_RESAMPLE 2   /* m ~ N(0,1) on resample          (models/dgp.py:210) */
+#define DGPRF_RNG_Z 3          /* z ~ N(0,1) RF frequencies       (layers/rf_layers.py:22) */
+#define DGPRF_RNG_W 4          /* W ~ N(0,1) GP weights           (layers/GP_weight_layers.py:9) */
+#define DGPRF_RNG_MOMENTS 5    /* initial momenta                 (models/dgp.py:240) */
+
+/* error codes */
+#define DGPRF_OK 0
+#define DGPRF_E_ARG -1         /* null pointer / bad scalar argument */
+#define DGPRF_E_SHAPE -2       /* unsupported shape (layers, widths, batch) */
+#define DGPRF_E_HIP -3         /* a HIP runtime call failed */
+#define DGPRF_E_PLAN -4        /* plan not initialised by dgprf_plan_init */
+
+/*
+ * Model plan.  Caller fills the first block (the DGP_RF constructor arguments,
+ * models/dgp.py:9-52 + the minibatch size and chain count); dgprf_plan_init derives the rest:
+ * per-layer widths (models/dgp.py:74-91), Phi widths (models/dgp.py:103,107), the packed
+ * parameter layout in HBM and the step-kernel workspace.
+ *
+ * Packed HBM layouts (floats):
+ *   theta / momenta [n_chains][w_total]  : W_l [P_l][g_l] at w_off[l]    (GPLayer.W, dgp.py:66-68)
+ *   z / omega       [omega_total]        : [d_l][R_l] at omega_off[l]    (RBFLayer.z / Omega)
+ *   hyp             [hyp_total]          : log_amp[L], lik_log_var, pad, log_inv_ls (sum d_l) at
+ *                                          lis_off[l], mean (sum d_l) at mean_off[l]
+ *   der             [der_total]          : c_l = amp/sqrt(R) (RBF) or sqrt2*amp/sqrt(R) (ARC),
+ *                                          then sigma^2 at der[DGPRF_MAX_LAYERS]
+ *   mass            [n_chains][n_layers] : preconditioner M per W_l (models/dgp.py:235-237)
+ *   workspace       [ws_total]           : step-kernel partials (per chain ws_chain floats)
+ */
+typedef struct dgprf_plan {
+  /* ---- caller ---- */
+  int32_t n_layers;
+  int32_t d_in;
+  int32_t d_out;
+  int32_t input_cat;
+  int32_t likelihood;
+  int32_t batch;        /* minibatch rows B the step kernels are sized for */
+  int32_t n_chains;     /* independent chains sharing Omega (one posterior) */
+  int32_t kind[DGPRF_MAX_LAYERS];
+  int32_t n_rf[DGPRF_MAX_LAYERS];
+  int32_t n_gp[DGPRF_MAX_LAYERS];
+  /* ---- derived by dgprf_plan_init ---- */
+  int32_t initialised;
+  int32_t d[DGPRF_MAX_LAYERS];      /* layer input width */
+  int32_t P[DGPRF_MAX_LAYERS];      /* Phi width: 2R (RBF) or R (ARC) */
+  int32_t ns[DGPRF_MAX_LAYERS];     /* feature slices per step kernel */
+  int32_t cpw[DGPRF_MAX_LAYERS];    /* 16-feature chunks per wave per slice */
+  int32_t n_row_tiles;              /* ceil(B/16) */
+  int32_t pad0;
+  int64_t omega_off[DGPRF_MAX_LAYERS];
+  int64_t w_off[DGPRF_MAX_LAYERS];
+  int64_t lis_off[DGPRF_MAX_LAYERS];
+  int64_t mean_off[DGPRF_MAX_LAYERS];
+  int64_t fp_off[DGPRF_MAX_LAYERS];  /* F partials  [ns][B][g]      (per chain) */
+  int64_t dxp_off[DGPRF_MAX_LAYERS]; /* dX partials [ns][B][g_{l-1}] (per chain, l>=1) */
+  int64_t gwp_off;                   /* gW partials [n_row_tiles][w_total] (per chain) */
+  int64_t logp_off;                  /* per-row minibatch log p [B] (per chain) */
+  int64_t omega_total;
+  int64_t w_total;
+  int64_t hyp_total;
+  int64_t der_total;
+  int64_t ws_chain;
+  int64_t ws_total;
+} dgprf_plan_t;
+
+/* Device state of the chains.  Replaces the tf.Variables W and their ad-hoc attributes
+ * `moments` and `M` (models/dgp.py:208-216, 235-240). */
+typedef struct dgprf_chain {
+  float *theta;          /* [C][w_total] */
+  float *mom;            /* [C][w_total] */
+  const float *omega;    /* [omega_total] (from dgprf_omega_build) */
+  const float *der;      /* [der_total]   (from dgprf_omega_build) */
+  const float *mass;     /* [C][n_layers] */
+  float *ws;             /* [ws_total] */
+  int64_t *step;         /* device step counter (Philox counter / minibatch position) */
+  uint64_t seed;         /* Philox key (already folded with the rank by the host) */
+} dgprf_chain_t;
+
+/* Minibatch source (replaces the host tf.data iterator, experiments/utils_dataset.py:26-44). */
+typedef struct dgprf_batch {
+  const float *X;        /* [n_data][d_in] */
+  const float *Y;        /* [n_data][y_cols] (softmax: class label as float in column 0) */
+  const int32_t *idx;    /* DGPRF_BATCH_INDEXED: [C][B] */
+  int64_t n_data;
+  int32_t y_cols;
+  int32_t mode;
+  int64_t iters_per_epoch;  /* DGPRF_BATCH_EPOCH: floor(n_data / B) */
+  uint64_t perm_seed;       /* DGPRF_BATCH_EPOCH */
+} dgprf_batch_t;
+
+/* One SGHMC/SGLD update's scalars: DGP_RF.sgmcmc_update(..., data_size, lr, momentum_decay,
+ * resample_moments, temperature) (models/dgp.py:184-216). */
+typedef struct dgprf_step {
+  float lr;
+  float momentum_decay;
+  float temperature;
+  float data_size;          /* N */
+  int32_t resample_moments;
+  int32_t schedule;         /* DGPRF_SCHED_* */
+  int32_t step_offset;      /* added to *chain.step (graph sub-step index) */
+  int32_t grad_only;        /* internal: set by dgprf_potential_grad */
+  /* DGPRF_SCHED_CYCLICAL (experiments/utils_training.py:47-61): */
+  int64_t start_step;       /* first sampling step (start_sampling_epoch * iters) */
+  int64_t cycle_length;     /* epochs_per_cycle * iters */
+  int32_t resample_in_cycle_head;
+  int32_t pad1;
+  /* optional injected standard normals (parity tests; NULL = device Philox): */
+  const float *xi;          /* [C][w_total] noise */
+  const float *xi_resample; /* [C][w_total] resampled momenta */
+} dgprf_step_t;
+
+typedef struct dgprf_graph *dgprf_graph_handle;
+
+/* ---------------- meta ---------------- */
+int dgprf_abi_version(void);
+const char *dgprf_error_string(int code);
+/* Derive the plan (models/dgp.py:34-115).  Host-only, no device work. */
+int dgprf_plan_init(dgprf_plan_t *plan);
+
+/* ---------------- initial draws ---------------- */
+/* Fill out[n] with N(0,1) from Philox4x32-10 (key = seed, counter = (i/4, sub_lo, sub_hi,
+ * purpose<<24)) + Box-Muller.  Replaces tf.random.normal at layers/rf_layers.py:22,
+ * layers/GP_weight_layers.py:9, models/dgp.py:210,212,240. */
+int dgprf_philox_normal(float *out, int64_t n, uint64_t seed, uint64_t subsequence,
+                        uint32_t purpose, void *stream);
+
+/* ---------------- kernel hyper-parameters ---------------- */
+/* Omega_l = exp(log_inv_ls_l)[:,None] * z_l + mean_l, c_l and sigma^2 into der.
+ * Replaces kernels/RBF.py:43-53, kernels/arc_cosine.py:46-56, layers/rf_layers.py:34-38,44,90,
+ * likelihoods/gaussian.py:14-16. */
+int dgprf_omega_build(const dgprf_plan_t *plan, const float *z, const float *hyp, float *omega,
+                      float *der, void *stream);
+
+/* ---------------- the hot path ---------------- */
+/* One full SGHMC/SGLD step for every chain: minibatch gather, forward through all L layers
+ * (Omega x -> cos|sin or relu -> Phi W), likelihood, analytic backward (gW_l = Phi_l^T dF_l +
+ * W_l/N), and the fused update with device Philox noise.  Advances *chain.step by one.
+ * Replaces DGP_RF.sgmcmc_update (models/dgp.py:184-216) with full_bayesian=False. */
+int dgprf_sghmc_step(const dgprf_plan_t *plan, const dgprf_chain_t *chain,
+                     const dgprf_batch_t *batch, const dgprf_step_t *step, void *stream);
+
+/* Gradient of U w.r.t. every W_l (models/dgp.py:161-182 + tape.gradient :194-198) into
+ * grad_out [C][w_total]; no update, step counter untouched. */
+int dgprf_potential_grad(const dgprf_plan_t *plan, const dgprf_chain_t *chain,
+                         const dgprf_batch_t *batch, float data_size, float *grad_out,
+                         void *stream);
+
+/* Capture `steps_per_graph` consecutive dgprf_sghmc_step calls (sub-step k uses
+ * step_offset = k, then *step += steps_per_graph) into one hipGraph. */
+int dgprf_graph_create_sghmc(dgprf_graph_handle *out, const dgprf_plan_t *plan,
+                             const dgprf_chain_t *chain, const dgprf_batch_t *batch,
+                             const dgprf_step_t *step, int32_t steps_per_graph);
+int dgprf_graph_launch(dgprf_graph_handle graph, void *stream);
+int dgprf_graph_destroy(dgprf_graph_handle graph);
+
+/* Per-kernel device time of one step, measured with hipEvents on `stream`: each of the 2L+1 step
+ * kernels (forward l = 0..L-1, backward l = 0..L-1, update) is launched `reps` times back to back
+ * and ms_out[k] receives its average milliseconds per launch.  Runs one full step first so the
+ * workspaces hold live data; advances the chain (the update kernel runs reps + 1 times). */
+int dgprf_profile_step(const dgprf_plan_t *plan, const dgprf_chain_t *chain,
+                       const dgprf_batch_t *batch, const dgprf_step_t *step, int32_t reps,
+                       float *ms_out, void *stream);
+
+/* ---------------- predictive / forward ---------------- */
+/* Forward of n rows through all layers for every chain (BNN_from_list.__call__, utils.py:10-16;
+ * BNN_from_list_input_cat.__call__, utils.py:32-44) plus the likelihood
+ * (RegressionDGP.eval_log_likelihood_and_se, models/regression_model.py:33-50;
+ * ClassificationDGP.eval_log_likelihood, models/classification_model.py:49-60).
+ * Optional outputs (NULL to skip), each with a per-chain stride of n rows:
+ *   f_out[l]  [C][n][g_l]   per-layer outputs (feed_forward_all_layers, regression_model.py:24-31)
+ *   logp      [C][n]        log p(y|F)
+ *   se        [C][n]        mean_k (y - f)^2 (Gaussian only)
+ *   lse_m/lse_s/se_sum [C][n]  online log-sum-exp over samples (experiments/utils_training.py:79-85)
+ *                         updated in place: m' = max(m, lp); s' = s e^{m-m'} + e^{lp-m'}.
+ * Y may be NULL when no likelihood output is requested. */
+int dgprf_forward(const dgprf_plan_t *plan, const float *theta, const float *omega,
+                  const float *der, const float *X, const float *Y, int32_t y_cols, int64_t n,
+                  float *const *f_out, float *logp, float *se, float *lse_m, float *lse_s,
+                  float *se_sum, void *stream);
+
+/* Posterior-predictive summary (experiments/utils_training.py:79-85):
+ * per point lse[n] = log sum_s exp(lp_s) over all chains' accumulators, and
+ * out[0] = mean_n(lse - log S_total) - log_y_std, out[1] = sqrt(sum se / (S_total n)) * y_std.
+ * lse_m/lse_s/se_sum are [parts][n] (chains x ranks), combined in fixed order. */
+int dgprf_lse_finalize(const float *lse_m, const float *lse_s, const float *se_sum,
+                       int32_t parts, int64_t n, double s_total, float log_y_std, float y_std,
+                       float *lse_out, double *out, void *stream);
+
+/* Omega and c of ONE stand-alone RF layer (RBFLayer / ARCLayer outside a DGP_RF):
+ * omega[d][R] = exp(log_inv_ls)[:,None] z + mean[:,None]; c[0] = amp/sqrt(R) or sqrt2 amp/sqrt(R).
+ * layers/rf_layers.py:34-44, 80-90; kernels/RBF.py:43-53. */
+int dgprf_rf_omega(int32_t kind, int32_t d, int32_t R, const float *z, const float *log_inv_ls,
+                   const float *mean, const float *log_amp, float *omega, float *c, void *stream);
+
+/* Single RF layer features (RBFLayer.__call__ layers/rf_layers.py:29-45, ARCLayer.__call__
+ * :75-91): phi[n][P] = c * [cos(XOmega) | sin(XOmega)] or c * relu(XOmega). */
+int dgprf_rf_features(int32_t kind, const float *X, int64_t n, int32_t d, const float *omega,
+                      int32_t R, const float *c, float *phi, void *stream);
+/* GPLayer.__call__ (layers/GP_weight_layers.py:11-15): F[n][g] = Phi[n][P] W[P][g]. */
+int dgprf_gp_matmul(const float *phi, int64_t n, int32_t P, const float *W, int32_t g, float *F,
+                    void *stream);
+
+/* sum log N(W;0,1) per chain (DGP_RF.prior_W, models/dgp.py:129-136) into out[C]. */
+int dgprf_prior_w(const dgprf_plan_t *plan, const float *theta, float *out, void *stream);
+
+/* ---------------- update / preconditioner ---------------- */
+/* Stand-alone SGHMC update of theta/mom from a given gradient grad [C][w_total]
+ * (models/dgp.py:206-216).  Uses *step + step->step_offset for the Philox counter. */
+int dgprf_sghmc_update(const dgprf_plan_t *plan, float *theta, float *mom, const float *grad,
+                       const float *mass, const int64_t *step_ctr, uint64_t seed,
+                       const dgprf_step_t *step, void *stream);
+/* Welford accumulation of one gradient sample (models/dgp.py:259-271):
+ * k is the 1-based sample index; mean/m2 [C][w_total]. */
+int dgprf_welford_update(const dgprf_plan_t *plan, const float *grad, float *mean, float *m2,
+                         int32_t k, void *stream);
+/* Per-layer mass estimate (models/dgp.py:276-288) into mass_est [C][L]:
+ * centered: sqrt(mean(m2/(K-1)) + 1e-7); else sqrt(mean(mean^2 + m2/K) + 1e-7). */
+int dgprf_mass_estimate(const dgprf_plan_t *plan, const float *mean, const float *m2,
+                        int32_t k_batches, int32_t centered, float *mass_est, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DGPRF_H */

@@ -1,0 +1,92 @@
+"""C-ABI checks that need no GPU: libdgprf.so loads, exports every entry point include/dgprf.h
+declares, the ctypes structs match the C layout (compiled with gcc), and dgprf_plan_init derives
+the reference's layer widths (models/dgp.py:74-115)."""
+import ctypes
+import json
+import os
+import re
+import subprocess
+
+import pytest
+
+from dgprf import _native as N
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(ROOT, "include", "dgprf.h")
+
+
+def declared_functions():
+    src = open(HDR).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(dgprf_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_exports_every_declared_symbol():
+    lib = N.lib()
+    names = declared_functions()
+    assert len(names) >= 18
+    for n in names:
+        assert hasattr(lib, n), n
+    assert set(names) == set(N.SIGNATURES), set(names) ^ set(N.SIGNATURES)
+    assert lib.dgprf_abi_version() == 1
+
+
+def test_struct_layout_matches_c(tmp_path):
+    structs = {"dgprf_plan_t": N.Plan, "dgprf_chain_t": N.Chain, "dgprf_batch_t": N.Batch,
+               "dgprf_step_t": N.Step}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HDR}"', 'int main(void){',
+             'printf("{");']
+    first = True
+    for cname, cls in structs.items():
+        for fname, _ in cls._fields_:
+            sep = "" if first else ","
+            first = False
+            lines.append(f'printf("{sep}\\"{cname}.{fname}\\": %zu", offsetof({cname}, {fname}));')
+        lines.append(f'printf(",\\"{cname}.sizeof\\": %zu", sizeof({cname}));')
+    lines += ['printf("}");', 'return 0;}']
+    c = tmp_path / "layout.c"
+    c.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.check_call(["gcc", "-std=c99", "-o", str(exe), str(c)])
+    got = json.loads(subprocess.check_output([str(exe)]).decode())
+    for cname, cls in structs.items():
+        assert got[f"{cname}.sizeof"] == ctypes.sizeof(cls), cname
+        for fname, _ in cls._fields_:
+            assert got[f"{cname}.{fname}"] == getattr(cls, fname).offset, (cname, fname)
+
+
+def test_plan_config2():
+    p = N.make_plan(8, 1, [N.RBF] * 3, [1024] * 3, [8, 8, 1], False, N.LIK_GAUSSIAN, 200, 1)
+    assert list(p.d[:3]) == [8, 8, 8] and list(p.P[:3]) == [2048] * 3
+    assert p.w_total == 2048 * 8 * 2 + 2048 and p.omega_total == 3 * 8 * 1024
+    assert p.n_row_tiles == 13 and list(p.ns[:3]) == [16] * 3
+    assert all(o % 4 == 0 for o in p.w_off[:3]) and p.ws_chain % 4 == 0
+
+
+def test_plan_input_cat_and_arc():
+    p = N.make_plan(13, 1, [N.RBF, N.ARC], [500, 300], [13, 1], True, N.LIK_GAUSSIAN, 200, 2)
+    assert list(p.d[:2]) == [13, 26]          # models/dgp.py:78-79
+    assert list(p.P[:2]) == [1000, 300]       # models/dgp.py:103,107
+    assert p.ws_total == 2 * p.ws_chain
+
+
+@pytest.mark.parametrize("bad", [
+    dict(kinds=[], n_rf=[], n_gp=[]),
+    dict(kinds=[0] * 9, n_rf=[8] * 9, n_gp=[2] * 9),
+    dict(kinds=[2], n_rf=[8], n_gp=[2]),
+    dict(kinds=[0], n_rf=[0], n_gp=[2]),
+    dict(kinds=[0], n_rf=[8], n_gp=[65]),
+])
+def test_plan_rejects_bad_configs(bad):
+    with pytest.raises((ValueError, RuntimeError)):
+        N.make_plan(4, 1, bad["kinds"], bad["n_rf"], bad["n_gp"], False, 0, 16, 1)
+
+
+def test_entry_points_validate_before_enqueue():
+    lib = N.lib()
+    assert lib.dgprf_sghmc_step(None, None, None, None, None) == N.E_ARG
+    p = N.Plan()  # not initialised
+    assert lib.dgprf_prior_w(ctypes.byref(p), None, None, None) == N.E_PLAN
+    assert lib.dgprf_rf_features(7, None, 0, 1, None, 1, None, None, None) == N.E_ARG
+    assert lib.dgprf_philox_normal(None, 4, 0, 0, 1, None) == N.E_ARG
+    assert lib.dgprf_error_string(N.E_SHAPE) == b"unsupported shape"

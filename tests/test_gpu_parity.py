@@ -1,0 +1,514 @@
+"""HIP path (libdgprf.so via the C-ABI) against the CPU oracle and the golden fixtures.
+
+Tolerances (fp32 device vs float64 oracle, stated per check): forward / log p rel 2e-5 of the
+output scale, gradients 1e-4 of the gradient scale, one update 1e-5; minibatch indices and
+graph-vs-eager replays bit-exact.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import dgp_oracle as O
+from oracle import rng as R
+
+pytestmark = pytest.mark.gpu
+
+KIND = {0: "RBF", 1: "ARC"}
+
+
+def rel_err(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    return float(np.max(np.abs(a - b)) / (np.max(np.abs(b)) + 1e-30))
+
+
+def cpu(t):
+    return t.detach().float().cpu().numpy()
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    from dgprf import _native as N
+    N.lib()
+    return torch.device("cuda", 0)
+
+
+def model_from_fixture(g):
+    from likelihoods import Gaussian, Softmax
+    from models.dgp import DGP_RF
+    L = len(g["kinds"])
+    d_in, d_out, cat, lik = (int(x) for x in g["dims"][:4])
+    likelihood = Gaussian(variance=float(np.exp(g["lik_log_var"]))) if lik == 0 else Softmax()
+    m = DGP_RF(d_in, d_out, n_hidden_layers=L, n_rf=[int(r) for r in g["n_rf"]],
+               n_gp=[int(x) for x in g["n_gp"]], likelihood=likelihood,
+               kernel_type_list=[KIND[int(k)] for k in g["kinds"]], input_cat=bool(cat),
+               set_nonzero_mean=True)
+    load_params(m, g)
+    return m
+
+
+def load_params(m, g, W_keys=None):
+    with torch.no_grad():
+        for l in range(m.n_hidden_layers):
+            rf, gp = m.BNN.layers[2 * l], m.BNN.layers[2 * l + 1]
+            rf.z.copy_(torch.as_tensor(g[f"z{l}"]))
+            rf.kernel.log_amplitude.copy_(torch.as_tensor(g[f"log_amp{l}"]))
+            rf.kernel.log_inv_length_scale.copy_(torch.as_tensor(g[f"log_inv_ls{l}"]))
+            rf.mean.copy_(torch.as_tensor(g[f"mean{l}"])[:, None])
+            gp.assign_W(g[(W_keys or "W{}").format(l)])
+        if hasattr(m.likelihood, "lik_log_var"):
+            m.likelihood.lik_log_var.copy_(torch.as_tensor(g["lik_log_var"]))
+
+
+def oracle_params(g):
+    L = len(g["kinds"])
+    d_in, d_out, cat, lik = (int(x) for x in g["dims"][:4])
+    return O.Params(d_in, d_out, list(g["n_rf"]), list(g["n_gp"]),
+                    [KIND[int(k)] for k in g["kinds"]], "gaussian" if lik == 0 else "softmax",
+                    bool(cat), z=[g[f"z{l}"] for l in range(L)], W=[g[f"W{l}"] for l in range(L)],
+                    log_amp=[g[f"log_amp{l}"] for l in range(L)],
+                    log_inv_ls=[g[f"log_inv_ls{l}"] for l in range(L)],
+                    mean=[g[f"mean{l}"] for l in range(L)], lik_log_var=g["lik_log_var"])
+
+
+def unpack(engine, flat, chain=0):
+    pl = engine.layout
+    out = []
+    for l in range(engine.L):
+        o, P, gg = pl.w_off[l], pl.P[l], pl.n_gp[l]
+        out.append(cpu(flat[chain, o:o + P * gg]).reshape(P, gg))
+    return out
+
+
+def pack(engine, per_layer):
+    t = torch.zeros(1, engine.layout.w_total, dtype=torch.float32)
+    pl = engine.layout
+    for l, a in enumerate(per_layer):
+        o = pl.w_off[l]
+        t[0, o:o + a.size] = torch.as_tensor(np.asarray(a, np.float32).reshape(-1))
+    return t.to(engine.dev)
+
+
+CASES = ["rbf2_gauss", "arc_rbf_softmax_cat", "mixed5", "wide_g"]
+
+
+# ----------------------------------------------------------------------------- RNG
+def test_philox_normal_matches_oracle(dev):
+    from dgprf import _native as N
+    from dgprf import engine as E
+    out = torch.empty(4099, dtype=torch.float32, device=dev)
+    N.call("dgprf_philox_normal", E.ptr(out), out.numel(), 0xABCDEF1234, 77, R.PURPOSE_Z,
+           E.stream())
+    ref = R.philox_normal(4099, 0xABCDEF1234, 77, R.PURPOSE_Z)
+    assert np.max(np.abs(cpu(out) - ref)) < 2e-5   # f32 log / sincospi vs float64
+
+
+# ----------------------------------------------------------------------------- layers
+@pytest.mark.parametrize("kind", ["RBF", "ARC"])
+@pytest.mark.parametrize("n,d,R_", [(37, 3, 20), (1, 5, 100), (130, 40, 33)])
+def test_rf_layer_standalone(dev, kind, n, d, R_):
+    from kernels import ARCKernel, RBFKernel
+    from layers import ARCLayer, GPLayer, RBFLayer
+    k = (RBFKernel if kind == "RBF" else ARCKernel)(n_feature=d, is_ard=True)
+    layer = (RBFLayer if kind == "RBF" else ARCLayer)(k, R_)
+    rng = np.random.default_rng(n + d)
+    with torch.no_grad():
+        k.log_amplitude.fill_(0.3)
+        k.log_inv_length_scale.copy_(torch.as_tensor(rng.normal(-0.5, 0.2, d)))
+    X = rng.standard_normal((n, d))
+    phi = cpu(layer(X))
+    p = O.Params(d, 1, [R_], [1], [kind], z=[cpu(layer.z)], log_amp=[0.3],
+                 log_inv_ls=[cpu(k.log_inv_length_scale)], mean=[np.zeros(d)])
+    _, ref = O.rf_features(p, 0, X)
+    assert phi.shape == ref.shape and rel_err(phi, ref) < 2e-5
+    gp = GPLayer(phi.shape[1], 3)
+    F = cpu(gp(torch.as_tensor(phi, device=dev)))
+    assert rel_err(F, phi.astype(np.float64) @ cpu(gp.W)) < 2e-5
+
+
+# ----------------------------------------------------------------------------- forward
+@pytest.mark.parametrize("name", CASES)
+def test_forward_and_likelihood(dev, golden, name):
+    g = golden(name)
+    m = model_from_fixture(g)
+    L = m.n_hidden_layers
+    F = cpu(m.BNN(g["X"]))
+    assert rel_err(F, g[f"F{L - 1}"]) < 2e-5
+    lp = cpu(m.log_likelihood(g["X"], g["Y"]))
+    assert np.max(np.abs(lp - g["logp"])) < 2e-5 * max(1.0, np.max(np.abs(g["logp"])))
+    U = float(m.U(g["X"], g["Y"], int(g["dims"][5])))
+    assert abs(U - float(g["U"])) < 2e-5 * max(1.0, abs(float(g["U"])))
+    assert abs(float(m.prior_W()) - float(g["prior_W"])) < 1e-5 * abs(float(g["prior_W"]))
+    if int(g["dims"][3]) == 0:
+        from models.regression_model import RegressionDGP
+        lp2, se = RegressionDGP.eval_log_likelihood_and_se(m, [(g["X"][:10], g["Y"][:10]),
+                                                               (g["X"][10:], g["Y"][10:])])
+        assert np.max(np.abs(cpu(lp2) - g["logp"])) < 2e-5 * max(1.0, np.max(np.abs(g["logp"])))
+        assert rel_err(cpu(se), g["se"]) < 5e-5
+        if not int(g["dims"][2]):
+            outs = RegressionDGP.feed_forward_all_layers(m, g["X"])
+            for l in range(L):
+                assert rel_err(cpu(outs[l]), g[f"F{l}"]) < 2e-5
+
+
+# ----------------------------------------------------------------------------- backward
+@pytest.mark.parametrize("name", CASES)
+def test_potential_grad(dev, golden, name):
+    g = golden(name)
+    m = model_from_fixture(g)
+    eng = m._engine
+    G = unpack(eng, eng.grad(g["X"], g["Y"], int(g["dims"][5])))
+    for l in range(m.n_hidden_layers):
+        assert rel_err(G[l], g[f"g{l}"]) < 1e-4, (name, l)
+
+
+@pytest.mark.parametrize("name", CASES)
+@pytest.mark.parametrize("resample", [False, True])
+def test_sghmc_step_injected_noise(dev, golden, name, resample):
+    g = golden(name)
+    m = model_from_fixture(g)
+    eng = m._engine
+    L = m.n_hidden_layers
+    lr, beta, T, N_ = g["step_scalars"]
+    with torch.no_grad():
+        for l in range(L):
+            eng.mom_view(l).copy_(torch.as_tensor(g[f"m0_{l}"]))
+        eng.mass[0, :L] = torch.as_tensor(g["M"], dtype=torch.float32)
+    eng.moments_ready = True
+    xi = pack(eng, [g[f"xi{l}"] for l in range(L)])
+    xr = pack(eng, [g[f"xr{l}"] for l in range(L)]) if resample else None
+    eng.step(g["X"], g["Y"], N_, lr, beta, T, resample=resample, xi=xi, xi_resample=xr)
+    sfx = "r" if resample else ""
+    for l in range(L):
+        assert rel_err(cpu(eng.W_view(l)), g[f"W1{sfx}_{l}"]) < 1e-5
+        assert rel_err(cpu(eng.mom_view(l)), g[f"m1{sfx}_{l}"]) < 1e-4
+
+
+def test_config1_sgld_trajectory(dev, golden):
+    """Config 1 (1-layer RBF n_rf=100, mcycle-shaped N=133, full batch): 50 SGLD steps with
+    injected noise track the float64 oracle trajectory."""
+    from likelihoods import Gaussian
+    from models.regression_model import RegressionDGP
+    g = golden("config1_sgld")
+    m = RegressionDGP(1, 1, n_hidden_layers=1, n_rf=100, n_gp=1,
+                      likelihood=Gaussian(variance=0.01), kernel_type_list=["RBF"])
+    with torch.no_grad():
+        m.BNN.layers[0].z.copy_(torch.as_tensor(g["z0"]))
+        m.BNN.layers[1].assign_W(g["W0"])
+        m.likelihood.lik_log_var.copy_(torch.as_tensor(g["lik_log_var"]))
+    m.precond_update(None, 133, precond_type="identity")
+    lr, beta, T, N_ = g["step_scalars"]
+    eng = m._engine
+    worst = 0.0
+    for t in range(g["xi"].shape[0]):
+        xi = pack(eng, [g["xi"][t]])
+        m._engine.step(g["X"], g["Y"], N_, lr, beta, T, xi=xi)
+        worst = max(worst, rel_err(cpu(eng.W_view(0)), g["traj"][t]))
+    assert worst < 1e-4
+
+
+def test_standalone_update(dev, golden):
+    g = golden("rbf2_gauss")
+    m = model_from_fixture(g)
+    eng = m._engine
+    lr, beta, T, N_ = g["step_scalars"]
+    eng.mass[0, :2] = torch.as_tensor(g["M"], dtype=torch.float32)
+    with torch.no_grad():
+        for l in range(2):
+            eng.mom_view(l).copy_(torch.as_tensor(g[f"m0_{l}"]))
+    grad = pack(eng, [g["g0"], g["g1"]])
+    xi = pack(eng, [g["xi0"], g["xi1"]])
+    eng.sghmc_update(grad, lr, beta, T, N_, xi=xi)
+    for l in range(2):
+        W1, m1 = O.sghmc_update(g[f"W{l}"], g[f"m0_{l}"], g[f"g{l}"], lr, N_, beta, T,
+                                g["M"][l], g[f"xi{l}"])
+        assert rel_err(cpu(eng.W_view(l)), W1) < 1e-6
+        assert rel_err(cpu(eng.mom_view(l)), m1) < 1e-5
+
+
+def test_device_philox_noise_counter(dev, golden):
+    """The update's in-kernel noise is the Philox stream (seed, sub = step, NOISE, tag = chain)
+    indexed by the packed element: a Philox step equals an injected-noise step."""
+    g = golden("mixed5")
+    a, b = model_from_fixture(g), model_from_fixture(g)
+    lr, beta, T, N_ = g["step_scalars"]
+    for mm in (a, b):
+        mm.precond_update(None, N_, precond_type="identity")
+        mm._engine.mom.zero_()
+        mm._engine.step_ctr.fill_(5)
+    a._engine.step(g["X"], g["Y"], N_, lr, beta, T)
+    eng = b._engine
+    xi = R.philox_normal(eng.layout.w_total, eng.seed, 5, R.PURPOSE_NOISE, tag=0)
+    eng.step(g["X"], g["Y"], N_, lr, beta, T,
+             xi=torch.as_tensor(xi, dtype=torch.float32)[None])
+    assert rel_err(cpu(a._engine.theta), cpu(eng.theta)) < 1e-5
+    assert int(a._engine.step_ctr) == 6
+
+
+# ----------------------------------------------------------------------------- minibatching
+def test_epoch_minibatch_rows_bit_exact(dev):
+    """DGPRF_BATCH_EPOCH rows (device Feistel) == oracle rows: the gradient of an EPOCH batch is
+    bitwise the gradient of the INDEXED batch with the oracle's indices."""
+    from likelihoods import Gaussian
+    from models.regression_model import RegressionDGP
+    m = RegressionDGP(3, 1, n_hidden_layers=2, n_rf=24, n_gp=[4, 1], likelihood=Gaussian())
+    eng = m._engine
+    n, B = 1037, 50
+    X = torch.randn(n, 3, device=dev)
+    Y = torch.randn(n, 1, device=dev)
+    iters = n // B
+    for t in (0, 7, iters - 1, iters, 3 * iters + 2):
+        eng.step_ctr.fill_(t)
+        ge = eng.grad(X, Y, n, batch_size=B, mode=2, perm_seed=99)
+        rows = R.batch_rows(t, B, n, iters, perm_seed=99)
+        gi = eng.grad(X, Y, n, batch_size=B, mode=1, idx=rows.astype(np.int32))
+        assert torch.equal(ge, gi), t
+        gd = eng.grad(X[torch.as_tensor(rows, device=dev)], Y[torch.as_tensor(rows, device=dev)], n)
+        assert torch.equal(ge, gd), t
+
+
+def test_graph_replay_equals_eager_steps(dev):
+    from likelihoods import Gaussian
+    from models.regression_model import RegressionDGP
+    from dgprf import engine as E
+    E.set_seed(11)
+    a = RegressionDGP(4, 1, n_hidden_layers=2, n_rf=40, n_gp=[3, 1], likelihood=Gaussian())
+    E.set_seed(11)
+    b = RegressionDGP(4, 1, n_hidden_layers=2, n_rf=40, n_gp=[3, 1], likelihood=Gaussian())
+    assert torch.equal(a._engine.theta, b._engine.theta)
+    n, B = 640, 64
+    X = torch.randn(n, 4, device=dev)
+    Y = torch.randn(n, 1, device=dev)
+    for mm in (a, b):
+        mm.precond_update(None, n, precond_type="identity")
+    b._engine.mom.copy_(a._engine.mom)
+    a.run_sgmcmc(X, Y, n, 24, batch_size=B, lr=0.01, momentum_decay=0.9, steps_per_graph=8,
+                 perm_seed=3)
+    for _ in range(24):
+        b._engine.step(X, Y, n, 0.01, 0.9, 1.0, batch_size=B, mode=2, perm_seed=3)
+    assert int(a._engine.step_ctr) == 24 == int(b._engine.step_ctr)
+    assert torch.equal(a._engine.theta, b._engine.theta)
+    assert torch.equal(a._engine.mom, b._engine.mom)
+
+
+def test_device_cyclical_schedule(dev):
+    """DGPRF_SCHED_CYCLICAL: burn-in lr0/T=0 then lr0 * rate^2, T=1 (utils_training.py:47-61)."""
+    from likelihoods import Gaussian
+    from models.regression_model import RegressionDGP
+    from dgprf import engine as E
+    from utils import cyclical_step_rate
+    E.set_seed(5)
+    a = RegressionDGP(2, 1, n_hidden_layers=1, n_rf=16, n_gp=1, likelihood=Gaussian())
+    E.set_seed(5)
+    b = RegressionDGP(2, 1, n_hidden_layers=1, n_rf=16, n_gp=1, likelihood=Gaussian())
+    n, B, start, cyc = 320, 32, 6, 5
+    X = torch.randn(n, 2, device=dev)
+    Y = torch.randn(n, 1, device=dev)
+    for mm in (a, b):
+        mm.precond_update(None, n, precond_type="identity")
+    b._engine.mom.copy_(a._engine.mom)
+    a.run_sgmcmc(X, Y, n, 16, batch_size=B, lr=0.05, momentum_decay=0.5, steps_per_graph=4,
+                 schedule="cyclical", start_step=start, cycle_length=cyc)
+    for t in range(16):
+        if t < start:
+            lr, T = 0.05, 0.0
+        else:
+            r, _ = cyclical_step_rate(t - start + 1, cyc, "cosine", min_value=0.0)
+            lr, T = float(np.float32(0.05) * (r * r)), 1.0
+        b._engine.step(X, Y, n, lr, 0.5, T, batch_size=B, mode=2)
+    assert rel_err(cpu(a._engine.theta), cpu(b._engine.theta)) < 1e-5
+
+
+def test_multichain_chain0_matches_single_chain(dev):
+    from dgprf import engine as E
+    from dgprf import _native as N
+    spec = E.ModelSpec(3, 1, [N.RBF, N.ARC], [32, 48], [4, 1], False, N.LIK_GAUSSIAN)
+    one, three = E.Engine(spec, 1, seed=42), E.Engine(spec, 3, seed=42)
+    one.draw_init()
+    three.z.copy_(one.z)
+    three.hyp.copy_(one.hyp)
+    three.theta.copy_(one.theta.expand(3, -1))
+    for e in (one, three):
+        e.mom.zero_()
+    n, B = 512, 64
+    X = torch.randn(n, 3, device=dev)
+    Y = torch.randn(n, 1, device=dev)
+    for e in (one, three):
+        e.build_omega()
+        e.graph(X, Y, B, n, 0.02, 0.9, 1.0, 6).launch()
+    assert torch.equal(one.theta[0], three.theta[0])
+    assert not torch.equal(three.theta[0], three.theta[1])
+    assert not torch.equal(three.theta[1], three.theta[2])
+
+
+# ----------------------------------------------------------------------------- predictive
+def test_predictive_lse_matches_oracle(dev, golden):
+    from likelihoods import Gaussian
+    from models.regression_model import RegressionDGP
+    from dgprf.predictive import PredictiveLSE
+    g = golden("predictive")
+    m = RegressionDGP(4, 1, n_hidden_layers=2, n_rf=[30, 30], n_gp=[5, 1],
+                      likelihood=Gaussian(variance=float(np.exp(g["lik_log_var"]))),
+                      set_nonzero_mean=True)
+    g2 = dict(g)
+    g2["kinds"] = np.array([0, 0])
+    load_params(m, g2)
+    acc = PredictiveLSE(m._engine, g["Xt"], g["Yt"])
+    S = g["logp"].shape[0]
+    for s in range(S):
+        m.assign_W([g[f"Ws{s}_0"], g[f"Ws{s}_1"]])
+        lp, se = m.eval_log_likelihood_and_se([(g["Xt"], g["Yt"])])
+        assert np.max(np.abs(cpu(lp) - g["logp"][s])) < 1e-4
+        acc.add_sample()
+    ll, rmse = acc.finalize(y_std=float(g["y_std"]))
+    assert abs(ll - float(g["LL"])) < 1e-4      # north_star: predictive log-lik within 1e-4
+    assert abs(rmse - float(g["RMSE"])) < 1e-5 * max(1.0, float(g["RMSE"]))
+
+
+def test_precond_rmsprop_masses(dev, golden):
+    from likelihoods import Gaussian
+    from models.regression_model import RegressionDGP
+    g = golden("precond")
+    for centered, key in ((False, "M"), (True, "M_centered")):
+        m = RegressionDGP(2, 1, n_hidden_layers=2, n_rf=[16, 24], n_gp=[3, 1],
+                          likelihood=Gaussian(variance=float(np.exp(g["lik_log_var"]))),
+                          set_nonzero_mean=True)
+        g2 = dict(g)
+        g2["kinds"] = np.array([0, 0])
+        load_params(m, g2)
+        m.precond_update(None, int(g["N"]), precond_type="identity")
+        m0 = cpu(m._engine.mom).copy()
+        ds = [(g["Xs"][k], g["Ys"][k]) for k in range(4)]
+        m.precond_update(ds, int(g["N"]), K_batches=4, second_moment_centered=centered)
+        M = cpu(m._engine.mass)[0]
+        assert rel_err(M, g[key]) < 1e-4
+        for l in range(2):   # moments = sqrt(M) * rsqrt(1) * moments_before
+            o, n_ = m._engine.layout.w_off[l], m._engine.layout.P[l] * m._engine.layout.n_gp[l]
+            assert rel_err(cpu(m._engine.mom)[0, o:o + n_], np.sqrt(M[l]) * m0[0, o:o + n_]) < 1e-5
+        with pytest.raises(AssertionError):
+            m.precond_update(ds[:2], int(g["N"]), K_batches=4)
+
+
+# ----------------------------------------------------------------------------- edge shapes
+@pytest.mark.parametrize("kinds,n_rf,n_gp,d_in,cat,lik,B", [
+    (["RBF"], [1], [1], 1, False, "gaussian", 1),            # smallest everything
+    (["RBF", "RBF"], [100, 17], [30, 2], 100, False, "gaussian", 33),  # large-d path, 2 out tiles
+    (["ARC", "RBF"], [64, 64], [16, 5], 40, True, "softmax", 200),      # input_cat, wide d
+    (["RBF"] * 3, [1024] * 3, [8, 8, 1], 8, False, "gaussian", 200),   # config 2 shapes
+])
+def test_edge_shapes_forward_and_grad(dev, kinds, n_rf, n_gp, d_in, cat, lik, B):
+    from likelihoods import Gaussian, Softmax
+    from models.dgp import DGP_RF
+    rng = np.random.default_rng(B + d_in)
+    d_out = n_gp[-1]
+    m = DGP_RF(d_in, d_out, n_hidden_layers=len(kinds), n_rf=n_rf, n_gp=n_gp,
+               likelihood=Gaussian() if lik == "gaussian" else Softmax(),
+               kernel_type_list=kinds, input_cat=cat)
+    p = O.Params(d_in, d_out, n_rf, n_gp, kinds, lik, cat,
+                 z=[cpu(m.BNN.layers[2 * l].z) for l in range(len(kinds))],
+                 W=[cpu(w) for w in m.W_mcmc],
+                 log_inv_ls=[cpu(k.log_inv_length_scale) for k in m.kernel_list],
+                 lik_log_var=np.log(0.1))
+    X = rng.standard_normal((B, d_in))
+    Y = rng.standard_normal((B, d_out)) if lik == "gaussian" else \
+        rng.integers(0, d_out, (B, 1)).astype(float)
+    assert rel_err(cpu(m.BNN(X)), O.forward(p, X)) < 5e-5
+    G = unpack(m._engine, m._engine.grad(X, Y, 10_000))
+    ref = O.grad_W(p, X, Y, 10_000)
+    for l in range(len(kinds)):
+        assert rel_err(G[l], ref[l]) < 2e-4, l
+
+
+def test_api_errors(dev):
+    from likelihoods import Gaussian
+    from models.regression_model import RegressionDGP
+    m = RegressionDGP(3, 1, n_hidden_layers=1, n_rf=8, n_gp=1, likelihood=Gaussian())
+    X, Y = np.zeros((4, 3), np.float32), np.zeros((4, 1), np.float32)
+    with pytest.raises(AssertionError, match="moments"):
+        m.sgmcmc_update(X, Y, 100)
+    m.precond_update(None, 100, precond_type="identity")
+    with pytest.raises(NotImplementedError):
+        m.sgmcmc_update(X, Y, 100, full_bayesian=True)
+    with pytest.raises(ValueError):
+        m.sgmcmc_update(np.zeros((4, 2), np.float32), Y, 100)
+    with pytest.raises(NotImplementedError):
+        m.precond_update(None, 100, precond_type="adam")
+    m.sgmcmc_update(X, Y, 100)   # works after precond_update
+    assert torch.isfinite(m._engine.theta).all()
+
+
+# ----------------------------------------------------------------------------- statistics
+@pytest.mark.parametrize("beta", [0.0, 0.9])
+def test_sampler_targets_gaussian_posterior(dev, beta):
+    """Full-batch SGLD / SGHMC on a 1-layer RF model (fixed features, Gaussian likelihood):
+    the posterior of W is N(mu, Sigma), Lambda = I + Phi^T Phi / s2, mu = Lambda^-1 Phi^T y / s2.
+    Sample moments from the device Philox-driven chain match it."""
+    from likelihoods import Gaussian
+    from models.regression_model import RegressionDGP
+    from dgprf import engine as E
+    E.set_seed(1000 + int(beta * 10))
+    n, R_, s2 = 64, 4, 0.5
+    m = RegressionDGP(1, 1, n_hidden_layers=1, n_rf=R_, n_gp=1, likelihood=Gaussian(variance=s2))
+    rng = np.random.default_rng(0)
+    X = rng.uniform(-2, 2, (n, 1))
+    Y = np.sin(2 * X) + 0.3 * rng.standard_normal((n, 1))
+    Phi = cpu(m.BNN.layers[0](X)).astype(np.float64)
+    Lam = np.eye(2 * R_) + Phi.T @ Phi / s2
+    Sig = np.linalg.inv(Lam)
+    mu = Sig @ Phi.T @ Y[:, 0] / s2
+    m.precond_update(None, n, precond_type="identity")
+    eps = 0.02 * np.min(np.diag(Sig))          # Langevin step h^2 = lr / N
+    lr = eps * n
+    Xd = torch.as_tensor(X, dtype=torch.float32, device=dev)
+    Yd = torch.as_tensor(Y, dtype=torch.float32, device=dev)
+    thin = 25
+    m.run_sgmcmc(Xd, Yd, n, 2000, batch_size=n, lr=lr, momentum_decay=beta, steps_per_graph=thin)
+    samples = []
+    for _ in range(2000):
+        m.run_sgmcmc(Xd, Yd, n, thin, batch_size=n, lr=lr, momentum_decay=beta,
+                     steps_per_graph=thin)
+        samples.append(m._engine.W_view(0)[:, 0].clone())
+    S = torch.stack(samples).double().cpu().numpy()
+    sd = np.sqrt(np.diag(Sig))
+    z = (S.mean(0) - mu) / sd
+    assert np.max(np.abs(z)) < 0.35, z                 # mean within 0.35 posterior sd
+    ratio = S.std(0) / sd
+    assert np.all((ratio > 0.8) & (ratio < 1.2)), ratio
+
+
+def test_full_config2_properties(dev):
+    """Config 2 at full size (N = 1e6, B = 200, L = 3, n_rf = 1024): one step's gradient vs the
+    float64 oracle on the same batch, deterministic replays, finite chains."""
+    from likelihoods import Gaussian
+    from models.regression_model import RegressionDGP
+    from dgprf import engine as E
+    from dgprf.data import regression_data
+    X, Y, _ = regression_data(1_000_000, 8, seed=0, device=dev)
+    runs = []
+    for rep in range(2):
+        E.set_seed(2)
+        m = RegressionDGP(8, 1, n_hidden_layers=3, n_rf=1024, n_gp=[8, 8, 1],
+                          likelihood=Gaussian(variance=0.1))
+        m.precond_update(None, 1_000_000, precond_type="identity")
+        if rep == 0:
+            eng = m._engine
+            eng.step_ctr.fill_(123)
+            G = unpack(eng, eng.grad(X, Y, 1_000_000, batch_size=200, mode=2, perm_seed=0))
+            rows = R.batch_rows(123, 200, 1_000_000, 5000, perm_seed=0)
+            p = O.Params(8, 1, [1024] * 3, [8, 8, 1], ["RBF"] * 3,
+                         z=[cpu(m.BNN.layers[2 * l].z) for l in range(3)],
+                         W=[cpu(w) for w in m.W_mcmc],
+                         log_inv_ls=[cpu(k.log_inv_length_scale) for k in m.kernel_list],
+                         lik_log_var=np.log(0.1))
+            ref = O.grad_W(p, cpu(X[torch.as_tensor(rows, device=dev)]),
+                           cpu(Y[torch.as_tensor(rows, device=dev)]), 1_000_000)
+            for l in range(3):
+                assert rel_err(G[l], ref[l]) < 1e-4
+            eng.step_ctr.fill_(0)
+        m.run_sgmcmc(X, Y, 1_000_000, 500, batch_size=200, lr=0.01, momentum_decay=0.9)
+        runs.append(m._engine.theta.clone())
+        assert torch.isfinite(runs[-1]).all()
+    assert torch.equal(runs[0], runs[1])
