@@ -183,21 +183,24 @@ int dgprf_plan_init(dgprf_plan_t* pl) {
   const int B = pl->batch;
   pl->n_row_tiles = (B + 15) / 16;
   int64_t ws = 0;
+  // partial buffers always hold DGPRF_NS_MAX slices / a multiple of 16 row tiles; the unused
+  // ones stay zero (caller zero-fills the workspace once) so consumers sum a fixed, unrolled
+  // count of independent loads in a fixed order.
   for (int l = 0; l < L; ++l) {
     pl->fp_off[l] = ws;
-    ws = align4(ws + (int64_t)pl->ns[l] * B * pl->n_gp[l]);
+    ws = align4(ws + (int64_t)DGPRF_NS_MAX * B * pl->n_gp[l]);
   }
   for (int l = 1; l < L; ++l) {
     pl->dxp_off[l] = ws;
-    ws = align4(ws + (int64_t)pl->ns[l] * B * pl->n_gp[l - 1]);
+    ws = align4(ws + (int64_t)DGPRF_NS_MAX * B * pl->n_gp[l - 1]);
   }
+  pl->n_rt_pad = (pl->n_row_tiles + 15) / 16 * 16;
   pl->gwp_off = ws;
-  ws = align4(ws + (int64_t)pl->n_row_tiles * pl->w_total);
+  ws = align4(ws + (int64_t)pl->n_rt_pad * pl->w_total);
   pl->logp_off = ws;
   ws = align4(ws + B);
   pl->ws_chain = ws;
   pl->ws_total = ws * pl->n_chains;
-  pl->pad0 = 0;
   pl->initialised = 1;
   return DGPRF_OK;
 }
@@ -318,28 +321,34 @@ int dgprf_profile_step(const dgprf_plan_t* plan, const dgprf_chain_t* chain,
   const hipStream_t s = as_stream(stream);
   dgprf_step_t st = *step;
   st.grad_only = 0;
-  const StepDev sd = make_step_dev(*plan, *chain, *batch, st.step_offset);
   const UpdateDev ud = make_update_dev(st);
-  hipError_t e = enqueue_step(*plan, sd, ud, s);
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  if (e == hipSuccess) e = hipEventCreate(&e0);
-  if (e == hipSuccess) e = hipEventCreate(&e1);
-  const int L = plan->n_layers;
-  for (int k = 0; k < 2 * L + 1 && e == hipSuccess; ++k) {
-    e = hipEventRecord(e0, s);
-    for (int r = 0; r < reps && e == hipSuccess; ++r) {
-      if (k < L) e = dgprf::launch_step_fwd(*plan, sd, k, s);
-      else if (k < 2 * L) e = dgprf::launch_step_bwd(*plan, sd, k - L, s);
+  const int L = plan->n_layers, K = 2 * L + 1;
+  hipEvent_t ev[2 * (2 * DGPRF_MAX_LAYERS + 1)] = {};
+  hipError_t e = hipSuccess;
+  for (int i = 0; i < 2 * K && e == hipSuccess; ++i) e = hipEventCreate(&ev[i]);
+  for (int k = 0; k < K; ++k) ms_out[k] = 0.f;
+  // the real step sequence (fwd 0..L-1, bwd L-1..0, update), every kernel between two events
+  for (int rep = 0; rep < reps && e == hipSuccess; ++rep) {
+    const StepDev sd = make_step_dev(*plan, *chain, *batch, st.step_offset);
+    for (int j = 0; j < K && e == hipSuccess; ++j) {
+      const int kk = j < L ? j : (j < 2 * L ? L + (2 * L - 1 - j) : 2 * L);
+      e = hipEventRecord(ev[2 * kk], s);
+      if (e != hipSuccess) break;
+      if (kk < L) e = dgprf::launch_step_fwd(*plan, sd, kk, s);
+      else if (kk < 2 * L) e = dgprf::launch_step_bwd(*plan, sd, kk - L, s);
       else e = dgprf::launch_step_update(*plan, sd, ud, nullptr, s);
+      if (e == hipSuccess) e = hipEventRecord(ev[2 * kk + 1], s);
     }
-    if (e == hipSuccess) e = hipEventRecord(e1, s);
-    if (e == hipSuccess) e = hipEventSynchronize(e1);
-    float ms = 0.f;
-    if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
-    ms_out[k] = ms / (float)reps;
+    if (e == hipSuccess) e = dgprf::launch_advance(chain->step, 1, s);
+    if (e == hipSuccess) e = hipEventSynchronize(ev[2 * (2 * L) + 1]);
+    for (int kk = 0; kk < K && e == hipSuccess; ++kk) {
+      float ms = 0.f;
+      e = hipEventElapsedTime(&ms, ev[2 * kk], ev[2 * kk + 1]);
+      ms_out[kk] += ms / (float)reps;
+    }
   }
-  if (e0) (void)hipEventDestroy(e0);
-  if (e1) (void)hipEventDestroy(e1);
+  for (int i = 0; i < 2 * K; ++i)
+    if (ev[i]) (void)hipEventDestroy(ev[i]);
   return hip_rc(e);
 }
 

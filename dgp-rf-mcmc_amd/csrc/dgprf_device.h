@@ -18,6 +18,7 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 
 #define DGPRF_WAVES 4
 #define DGPRF_TILE_ROWS 16
+#define DGPRF_NS_MAX 16  // feature slices per step kernel (partial buffers are padded to it)
 
 __device__ __forceinline__ f4 mfma16(float a, float b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);

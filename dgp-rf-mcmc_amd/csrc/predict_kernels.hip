@@ -44,9 +44,118 @@ struct FOut {
   float* p[DGPRF_MAX_LAYERS];
 };
 
+// One wave's F partial of one layer over its features (chunks wave, wave+4, ...), written to
+// red[wave][16][NOT*16].  Fragments of the next chunk are loaded before the current chunk's MFMAs;
+// cos and sin products accumulate in separate chains.  G1 (g == 1): the W^T Phi^T product is a
+// per-lane dot product (VALU) reduced over the 4 lane groups, instead of a 16x16 MFMA tile that
+// would be 15/16 padding.
+template <bool SMALLD, int NOT, bool RBF, bool G1>
+__device__ __forceinline__ void layer_partial(const float* __restrict__ om,
+                                              const float* __restrict__ W, int R, int d, int g,
+                                              float cl, const float* xs, int xst, float* red,
+                                              int wave, int lr, int lq) {
+  float xf[8];
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) xf[ks] = (SMALLD && 4 * ks < d) ? xs[lr * xst + 4 * ks + lq] : 0.f;
+  float omk[8], wf[NOT][4][2];
+  auto load_frag = [&](int f0) {
+    const int fa = f0 + lr;
+    if (SMALLD) {
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        const int k = 4 * ks + lq;
+        omk[ks] = (4 * ks < d && fa < R && k < d) ? om[(int64_t)k * R + fa] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int ot = 0; ot < NOT; ++ot) {
+      const int o = G1 ? 0 : ot * 16 + lr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int fr = f0 + 4 * lq + r;
+        const bool ok = o < g && fr < R;
+        wf[ot][r][0] = ok ? W[(int64_t)fr * g + o] : 0.f;
+        wf[ot][r][1] = (RBF && ok) ? W[(int64_t)(R + fr) * g + o] : 0.f;
+      }
+    }
+  };
+  f4 acc[NOT], acs[NOT];
+#pragma unroll
+  for (int ot = 0; ot < NOT; ++ot) acc[ot] = acs[ot] = f4zero();
+  float dot = 0.f;
+  int f0 = wave * 16;
+  if (f0 < R) load_frag(f0);
+  for (; f0 < R; f0 += NW * 16) {
+    f4 at = f4zero();
+    if (SMALLD) {
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks)
+        if (4 * ks < d) at = mfma16(omk[ks], xf[ks], at);
+    } else {
+      const int fa = f0 + lr;
+      const int KS = round4(d) >> 2;
+      for (int ks = 0; ks < KS; ++ks) {
+        const int k = 4 * ks + lq;
+        const float o = (fa < R && k < d) ? om[(int64_t)k * R + fa] : 0.f;
+        at = mfma16(o, xs[lr * xst + 4 * ks + lq], at);
+      }
+    }
+    float p0[4], p1[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (RBF) {
+        float s, c;
+        rf_sincos(at[r], &s, &c);
+        p0[r] = cl * c;
+        p1[r] = cl * s;
+      } else {
+        p0[r] = cl * fmaxf(at[r], 0.f);
+        p1[r] = 0.f;
+      }
+    }
+    float wcur[NOT][4][2];
+#pragma unroll
+    for (int ot = 0; ot < NOT; ++ot)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        wcur[ot][r][0] = wf[ot][r][0];
+        wcur[ot][r][1] = wf[ot][r][1];
+      }
+    if (f0 + NW * 16 < R) load_frag(f0 + NW * 16);  // prefetch next chunk
+    if (G1) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        dot = fmaf(p0[r], wcur[0][r][0], dot);
+        if (RBF) dot = fmaf(p1[r], wcur[0][r][1], dot);
+      }
+    } else {
+#pragma unroll
+      for (int ot = 0; ot < NOT; ++ot)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          acc[ot] = mfma16(wcur[ot][r][0], p0[r], acc[ot]);
+          if (RBF) acs[ot] = mfma16(wcur[ot][r][1], p1[r], acs[ot]);
+        }
+    }
+  }
+  constexpr int GP = NOT * 16;
+  float* redw = red + wave * TR * GP;
+  if (G1) {
+    dot += __shfl_xor(dot, 16);
+    dot += __shfl_xor(dot, 32);
+    if (lq == 0) redw[lr * GP] = dot;
+  } else {
+    // acc[ot][r] = F partial[row lr][ot*16 + 4lq + r]
+#pragma unroll
+    for (int ot = 0; ot < NOT; ++ot)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) redw[lr * GP + ot * 16 + 4 * lq + r] = acc[ot][r] + acs[ot][r];
+  }
+}
+
 // One workgroup = one 16-row tile; its 4 waves split each layer's RF features (16-feature chunks
 // w, w+4, ...) and the per-wave F partials are summed in LDS in wave order.
-template <bool SMALLD>
+template <bool SMALLD, int NOTMAX>
 __global__ __launch_bounds__(256) void k_forward_rows(
     const dgprf_plan_t pl, const float* __restrict__ theta, const float* __restrict__ omega,
     const float* __restrict__ der, const float* __restrict__ X, const float* __restrict__ Y,
@@ -77,78 +186,31 @@ __global__ __launch_bounds__(256) void k_forward_rows(
     }
     __syncthreads();
 
-    const bool rbf = pl.kind[layer] == DGPRF_RBF;
-    const float* __restrict__ om = omega + pl.omega_off[layer];
-    const float* __restrict__ W = Wc + pl.w_off[layer];
-    const float cl = der[layer];
-    const int NOT = (g + 15) >> 4;
-    float xf[8];
-    if (SMALLD) {
-#pragma unroll
-      for (int ks = 0; ks < 8; ++ks) xf[ks] = (4 * ks < d) ? xs[lr * LD.xst + 4 * ks + lq] : 0.f;
-    }
-    f4 acc[4] = {f4zero(), f4zero(), f4zero(), f4zero()};
-    for (int f0 = wave * 16; f0 < R; f0 += NW * 16) {
-      const int fa = f0 + lr;
-      const bool fok = fa < R;
-      f4 at = f4zero();
-      if (SMALLD) {
-#pragma unroll
-        for (int ks = 0; ks < 8; ++ks) {
-          if (4 * ks < d) {
-            const int k = 4 * ks + lq;
-            const float o = (fok && k < d) ? om[(int64_t)k * R + fa] : 0.f;
-            at = mfma16(o, xf[ks], at);
-          }
-        }
-      } else {
-        const int KS = dpad >> 2;
-        for (int ks = 0; ks < KS; ++ks) {
-          const int k = 4 * ks + lq;
-          const float o = (fok && k < d) ? om[(int64_t)k * R + fa] : 0.f;
-          at = mfma16(o, xs[lr * LD.xst + 4 * ks + lq], at);
-        }
-      }
-      float p0[4], p1[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (rbf) {
-          float s, c;
-          rf_sincos(at[r], &s, &c);
-          p0[r] = cl * c;
-          p1[r] = cl * s;
-        } else {
-          p0[r] = cl * fmaxf(at[r], 0.f);
-          p1[r] = 0.f;
-        }
-      }
-#pragma unroll
-      for (int ot = 0; ot < 4; ++ot) {
-        if (ot < NOT) {
-          const int o = ot * 16 + lr;
-          const bool ook = o < g;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int fr = f0 + 4 * lq + r;
-            const bool ok = ook && fr < R;
-            const float wc = ok ? W[(int64_t)fr * g + o] : 0.f;
-            acc[ot] = mfma16(wc, p0[r], acc[ot]);
-            if (rbf) {
-              const float wsn = ok ? W[(int64_t)(R + fr) * g + o] : 0.f;
-              acc[ot] = mfma16(wsn, p1[r], acc[ot]);
-            }
-          }
-        }
+    {
+      const float* __restrict__ om = omega + pl.omega_off[layer];
+      const float* __restrict__ W = Wc + pl.w_off[layer];
+      const float cl = der[layer];
+      const int NOT = (g + 15) >> 4;
+      const bool rbf = pl.kind[layer] == DGPRF_RBF;
+      // runtime (layer) -> compile-time body: output tiles, kernel kind, g == 1 VALU path
+      if (g == 1) {
+        if (rbf) layer_partial<SMALLD, 1, true, true>(om, W, R, d, g, cl, xs, LD.xst, red, wave, lr, lq);
+        else layer_partial<SMALLD, 1, false, true>(om, W, R, d, g, cl, xs, LD.xst, red, wave, lr, lq);
+      } else if (NOT == 1) {
+        if (rbf) layer_partial<SMALLD, 1, true, false>(om, W, R, d, g, cl, xs, LD.xst, red, wave, lr, lq);
+        else layer_partial<SMALLD, 1, false, false>(om, W, R, d, g, cl, xs, LD.xst, red, wave, lr, lq);
+      } else if (NOTMAX >= 2 && NOT == 2) {
+        if (rbf) layer_partial<SMALLD, (NOTMAX >= 2 ? 2 : 1), true, false>(om, W, R, d, g, cl, xs, LD.xst, red, wave, lr, lq);
+        else layer_partial<SMALLD, (NOTMAX >= 2 ? 2 : 1), false, false>(om, W, R, d, g, cl, xs, LD.xst, red, wave, lr, lq);
+      } else if (NOTMAX >= 3 && NOT == 3) {
+        if (rbf) layer_partial<SMALLD, (NOTMAX >= 3 ? 3 : 1), true, false>(om, W, R, d, g, cl, xs, LD.xst, red, wave, lr, lq);
+        else layer_partial<SMALLD, (NOTMAX >= 3 ? 3 : 1), false, false>(om, W, R, d, g, cl, xs, LD.xst, red, wave, lr, lq);
+      } else if (NOTMAX >= 4) {
+        if (rbf) layer_partial<SMALLD, (NOTMAX >= 4 ? 4 : 1), true, false>(om, W, R, d, g, cl, xs, LD.xst, red, wave, lr, lq);
+        else layer_partial<SMALLD, (NOTMAX >= 4 ? 4 : 1), false, false>(om, W, R, d, g, cl, xs, LD.xst, red, wave, lr, lq);
       }
     }
-    // acc[ot][r] = F partial[row lr][ot*16 + 4lq + r] of this wave's features
-    const int GP = NOT * 16;
-    float* redw = red + wave * TR * GP;
-#pragma unroll
-    for (int ot = 0; ot < 4; ++ot)
-      if (ot < NOT)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) redw[lr * GP + ot * 16 + 4 * lq + r] = acc[ot][r];
+    const int GP = ((g + 15) >> 4) * 16;
     __syncthreads();
     float* out = fo.p[layer] ? fo.p[layer] + (int64_t)chain * n * g : nullptr;
     for (int e = threadIdx.x; e < TR * g; e += blockDim.x) {
@@ -332,18 +394,29 @@ hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const
   FOut fo;
   for (int l = 0; l < DGPRF_MAX_LAYERS; ++l) fo.p[l] = (f_out && l < pl.n_layers) ? f_out[l] : nullptr;
   bool smalld = true;
-  for (int l = 0; l < pl.n_layers; ++l) smalld = smalld && pl.d[l] <= 32;
+  int notmax = 1;
+  for (int l = 0; l < pl.n_layers; ++l) {
+    smalld = smalld && pl.d[l] <= 32;
+    notmax = max(notmax, (pl.n_gp[l] + 15) >> 4);
+  }
   dim3 grid((unsigned)((n + TR - 1) / TR), pl.n_chains);
   const size_t lds = (size_t)LD.total * sizeof(float);
+#define DGPRF_FWD_LAUNCH(S, NM)                                                                    \
+  do {                                                                                             \
+    set_lds_limit((const void*)k_forward_rows<S, NM>, lds);                                        \
+    hipLaunchKernelGGL((k_forward_rows<S, NM>), grid, dim3(256), lds, s, pl, theta, omega, der, X, \
+                       Y, y_cols, n, fo, logp, se, lse_m, lse_s, se_sum);                          \
+  } while (0)
   if (smalld) {
-    set_lds_limit((const void*)k_forward_rows<true>, lds);
-    hipLaunchKernelGGL(k_forward_rows<true>, grid, dim3(256), lds, s, pl, theta, omega, der, X, Y,
-                       y_cols, n, fo, logp, se, lse_m, lse_s, se_sum);
+    if (notmax == 1) DGPRF_FWD_LAUNCH(true, 1);
+    else if (notmax == 2) DGPRF_FWD_LAUNCH(true, 2);
+    else DGPRF_FWD_LAUNCH(true, 4);
   } else {
-    set_lds_limit((const void*)k_forward_rows<false>, lds);
-    hipLaunchKernelGGL(k_forward_rows<false>, grid, dim3(256), lds, s, pl, theta, omega, der, X, Y,
-                       y_cols, n, fo, logp, se, lse_m, lse_s, se_sum);
+    if (notmax == 1) DGPRF_FWD_LAUNCH(false, 1);
+    else if (notmax == 2) DGPRF_FWD_LAUNCH(false, 2);
+    else DGPRF_FWD_LAUNCH(false, 4);
   }
+#undef DGPRF_FWD_LAUNCH
   return hipGetLastError();
 }
 

@@ -15,15 +15,19 @@
 //     gW[f][o]   = Phi^T dF               (K = batch rows; A recomputed in row-major orientation)
 //     dPhi[f][b] = W dF^T                 (K = g_l)
 //     dX^T[k][b] = Omega dA^T             (K = features)
-//   Cross-slice sums of F / dX partials are done by the CONSUMING kernel's prologue in a fixed
-//   order (deterministic, no atomics); the gW partials of the row tiles are summed by the update
-//   kernel, which also applies the prior term W/N and the SGHMC update with Philox noise.
+//   Cross-slice sums of F / dX partials are done by the CONSUMING kernel's prologue: always
+//   DGPRF_NS_MAX slices (unused ones are zero) as one unrolled burst of independent loads summed in
+//   a fixed order — deterministic, no atomics, one memory round trip.  The gW partials of the row
+//   tiles are summed the same way by the update kernel, which also applies the prior term W/N and
+//   the SGHMC update with Philox noise.  Omega/W fragments of a wave's first chunk are loaded
+//   before the dependent partial sums so both latencies overlap.
 #include "dgprf_internal.h"
 
 namespace {
 
 constexpr int NW = DGPRF_WAVES;
 constexpr int TR = DGPRF_TILE_ROWS;
+constexpr int NSM = DGPRF_NS_MAX;
 constexpr float LOG_2PI = 1.8378770664093453f;
 
 __device__ __forceinline__ int64_t cur_step(const StepDev& sd) {
@@ -31,6 +35,17 @@ __device__ __forceinline__ int64_t cur_step(const StepDev& sd) {
 }
 
 __host__ __device__ __forceinline__ int round4(int x) { return (x + 3) & ~3; }
+
+// sum over the DGPRF_NS_MAX slices of a partial buffer: independent loads, fixed order.
+__device__ __forceinline__ float sum_slices(const float* __restrict__ p, int64_t stride) {
+  float v[NSM];
+#pragma unroll
+  for (int s = 0; s < NSM; ++s) v[s] = p[s * stride];
+  float acc = v[0];
+#pragma unroll
+  for (int s = 1; s < NSM; ++s) acc += v[s];
+  return acc;
+}
 
 // LDS carve of a step kernel (floats):  ridx (16 x int64) | xs [16][xst] | aux [16][auxst] | red
 struct StepLds {
@@ -48,6 +63,11 @@ __host__ __device__ inline StepLds step_lds(const dgprf_plan_t& pl, int layer) {
   return L;
 }
 
+// Does layer `layer`'s X tile need dataset rows?  (layer 0, or input_cat concatenation)
+__device__ __forceinline__ bool needs_rows(const dgprf_plan_t& pl, int layer) {
+  return layer == 0 || pl.input_cat;
+}
+
 // Build the layer-`layer` input tile X_l[16][d_l] of batch rows row0.. into xs.
 //   layer 0: minibatch rows of the dataset; layer l>0: sum over slices of F_{l-1} partials
 //   (+ the dataset row for input_cat, [F | X] order of utils.py:42).
@@ -56,20 +76,14 @@ __device__ void load_x_tile(const dgprf_plan_t& pl, const StepDev& sd, int layer
   const int d = pl.d[layer], dpad = round4(d), B = pl.batch;
   const float* wsc = sd.ws + (int64_t)chain * pl.ws_chain;
   const int gp = layer > 0 ? pl.n_gp[layer - 1] : 0;
-  const int nsp = layer > 0 ? pl.ns[layer - 1] : 0;
   for (int e = threadIdx.x; e < TR * dpad; e += blockDim.x) {
     const int r = e / dpad, k = e - r * dpad, b = row0 + r;
     float v = 0.f;
     if (b < B && k < d) {
-      if (k < gp) {
-        const float* fp = wsc + pl.fp_off[layer - 1] + (int64_t)b * gp + k;
-        const int64_t ss = (int64_t)B * gp;
-        float acc = 0.f;
-        for (int s = 0; s < nsp; ++s) acc += fp[s * ss];
-        v = acc;
-      } else {
+      if (k < gp)
+        v = sum_slices(wsc + pl.fp_off[layer - 1] + (int64_t)b * gp + k, (int64_t)B * gp);
+      else
         v = sd.bd.X[ridx[r] * pl.d_in + (k - gp)];
-      }
     }
     xs[r * xst + k] = v;
   }
@@ -83,24 +97,31 @@ __device__ __forceinline__ void fill_ridx(const dgprf_plan_t& pl, const StepDev&
   }
 }
 
-// A-tile of 16 features x 16 rows.  TRANS=false: at[r] = A[row lr][f0+4lq+r]   (features in regs)
-//                                    TRANS=true : at[r] = A[row 4lq+r][f0+lr]   (rows in regs)
+// Omega fragments of one 16-feature chunk: om_k[ks] = Omega[4ks+lq][f0+lr] (SMALLD: d <= 32).
+__device__ __forceinline__ void load_om_frag(const float* __restrict__ om, int R, int d, int f0,
+                                             int lr, int lq, float (&omk)[8]) {
+  const int fa = f0 + lr;
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) {
+    const int k = 4 * ks + lq;
+    omk[ks] = (4 * ks < d && fa < R && k < d) ? om[(int64_t)k * R + fa] : 0.f;
+  }
+}
+
+// A-tile from fragments.  TRANS=false: at[r] = A[row lr][f0+4lq+r]   (features in regs)
+//                         TRANS=true : at[r] = A[row 4lq+r][f0+lr]   (rows in regs)
 template <bool SMALLD, bool TRANS>
 __device__ __forceinline__ f4 a_tile(const float* __restrict__ om, int R, int d, int f0,
-                                     const float* xf, const float* xs, int xst, int lr, int lq) {
+                                     const float (&omk)[8], const float (&xf)[8],
+                                     const float* xs, int xst, int lr, int lq) {
   f4 at = f4zero();
-  const int fa = f0 + lr;
-  const bool fok = fa < R;
   if (SMALLD) {
 #pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
-      const int k = 4 * ks + lq;
-      if (4 * ks < d) {
-        const float o = (fok && k < d) ? om[(int64_t)k * R + fa] : 0.f;
-        at = TRANS ? mfma16(xf[ks], o, at) : mfma16(o, xf[ks], at);
-      }
-    }
+    for (int ks = 0; ks < 8; ++ks)
+      if (4 * ks < d) at = TRANS ? mfma16(xf[ks], omk[ks], at) : mfma16(omk[ks], xf[ks], at);
   } else {
+    const int fa = f0 + lr;
+    const bool fok = fa < R;
     const int KS = round4(d) >> 2;
     for (int ks = 0; ks < KS; ++ks) {
       const int k = 4 * ks + lq;
@@ -112,8 +133,41 @@ __device__ __forceinline__ f4 a_tile(const float* __restrict__ om, int R, int d,
   return at;
 }
 
+template <bool RBF>
+__device__ __forceinline__ void features(const f4 at, float cl, float (&p0)[4], float (&p1)[4]) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    if (RBF) {
+      float s, c;
+      rf_sincos(at[r], &s, &c);
+      p0[r] = cl * c;
+      p1[r] = cl * s;
+    } else {
+      p0[r] = cl * fmaxf(at[r], 0.f);
+      p1[r] = 0.f;
+    }
+  }
+}
+
+// W fragments for F^T += W^T Phi^T: wf[ot][r][0|1] = W[f0+4lq+r (| R+...)][ot*16+lr]
+template <int NOT, bool RBF>
+__device__ __forceinline__ void load_w_frag(const float* __restrict__ W, int R, int g, int f0,
+                                            int lr, int lq, float (&wf)[NOT][4][2]) {
+#pragma unroll
+  for (int ot = 0; ot < NOT; ++ot) {
+    const int o = ot * 16 + lr;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int fr = f0 + 4 * lq + r;
+      const bool ok = o < g && fr < R;
+      wf[ot][r][0] = ok ? W[(int64_t)fr * g + o] : 0.f;
+      wf[ot][r][1] = (RBF && ok) ? W[(int64_t)(R + fr) * g + o] : 0.f;
+    }
+  }
+}
+
 // ------------------------------------------------------------------------- forward
-template <bool SMALLD>
+template <bool SMALLD, int NOT, bool RBF>
 __global__ __launch_bounds__(256) void k_step_fwd(const dgprf_plan_t pl, const StepDev sd,
                                                   const int layer) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -122,74 +176,59 @@ __global__ __launch_bounds__(256) void k_step_fwd(const dgprf_plan_t pl, const S
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, lr = lane & 15, lq = lane >> 4;
   const int d = pl.d[layer], R = pl.n_rf[layer], g = pl.n_gp[layer], B = pl.batch;
   const int row0 = rt * TR;
-  const int64_t t = cur_step(sd);
   int64_t* ridx = reinterpret_cast<int64_t*>(smem);
   float* xs = smem + 32;
   float* red = smem + LD.red_off;
+  const float* __restrict__ om = sd.omega + pl.omega_off[layer];
+  const float* __restrict__ W = sd.theta + (int64_t)chain * pl.w_total + pl.w_off[layer];
+  const int cpw = pl.cpw[layer];
+  auto chunk_f0 = [&](int i) { return ((sl * cpw + i) * NW + wave) * 16; };
 
-  fill_ridx(pl, sd, chain, row0, t, ridx);
-  __syncthreads();
+  // prefetch the first chunk's fragments (independent of the X tile)
+  float omk[8], wf[NOT][4][2];
+  if (SMALLD) load_om_frag(om, R, d, chunk_f0(0), lr, lq, omk);
+  load_w_frag<NOT, RBF>(W, R, g, chunk_f0(0), lr, lq, wf);
+  const float cl = sd.der[layer];
+
+  if (needs_rows(pl, layer)) {
+    fill_ridx(pl, sd, chain, row0, cur_step(sd), ridx);
+    __syncthreads();
+  }
   load_x_tile(pl, sd, layer, chain, row0, ridx, xs, LD.xst);
   __syncthreads();
 
-  const bool rbf = pl.kind[layer] == DGPRF_RBF;
-  const float* __restrict__ om = sd.omega + pl.omega_off[layer];
-  const float* __restrict__ W = sd.theta + (int64_t)chain * pl.w_total + pl.w_off[layer];
-  const float cl = sd.der[layer];
-  const int NOT = (g + 15) >> 4;
-
   float xf[8];
-  if (SMALLD) {
 #pragma unroll
-    for (int ks = 0; ks < 8; ++ks) xf[ks] = (4 * ks < d) ? xs[lr * LD.xst + 4 * ks + lq] : 0.f;
-  }
+  for (int ks = 0; ks < 8; ++ks) xf[ks] = (SMALLD && 4 * ks < d) ? xs[lr * LD.xst + 4 * ks + lq] : 0.f;
 
-  f4 acc[4] = {f4zero(), f4zero(), f4zero(), f4zero()};
-  const int cpw = pl.cpw[layer];
+  f4 acc[NOT], acs[NOT];
+#pragma unroll
+  for (int ot = 0; ot < NOT; ++ot) acc[ot] = acs[ot] = f4zero();
   for (int i = 0; i < cpw; ++i) {
-    const int f0 = ((sl * cpw + i) * NW + wave) * 16;
+    const int f0 = chunk_f0(i);
     if (f0 >= R) break;
-    const f4 at = a_tile<SMALLD, false>(om, R, d, f0, xf, xs, LD.xst, lr, lq);
+    const f4 at = a_tile<SMALLD, false>(om, R, d, f0, omk, xf, xs, LD.xst, lr, lq);
     float p0[4], p1[4];
+    features<RBF>(at, cl, p0, p1);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      if (rbf) {
-        float s, c;
-        rf_sincos(at[r], &s, &c);
-        p0[r] = cl * c;
-        p1[r] = cl * s;
-      } else {
-        p0[r] = cl * fmaxf(at[r], 0.f);
-        p1[r] = 0.f;
+    for (int ot = 0; ot < NOT; ++ot)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        acc[ot] = mfma16(wf[ot][r][0], p0[r], acc[ot]);
+        if (RBF) acs[ot] = mfma16(wf[ot][r][1], p1[r], acs[ot]);
       }
-    }
-#pragma unroll
-    for (int ot = 0; ot < 4; ++ot) {
-      if (ot < NOT) {
-        const int o = ot * 16 + lr;
-        const bool ook = o < g;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int fr = f0 + 4 * lq + r;
-          const bool ok = ook && fr < R;
-          const float wc = ok ? W[(int64_t)fr * g + o] : 0.f;
-          acc[ot] = mfma16(wc, p0[r], acc[ot]);
-          if (rbf) {
-            const float wsn = ok ? W[(int64_t)(R + fr) * g + o] : 0.f;
-            acc[ot] = mfma16(wsn, p1[r], acc[ot]);
-          }
-        }
-      }
+    if (i + 1 < cpw && chunk_f0(i + 1) < R) {
+      if (SMALLD) load_om_frag(om, R, d, chunk_f0(i + 1), lr, lq, omk);
+      load_w_frag<NOT, RBF>(W, R, g, chunk_f0(i + 1), lr, lq, wf);
     }
   }
   // acc[ot][r] = F[row lr][ot*16 + 4lq + r]; sum the 4 waves' feature chunks in LDS.
-  const int GP = NOT * 16;
+  constexpr int GP = NOT * 16;
   float* redw = red + wave * TR * GP;
 #pragma unroll
-  for (int ot = 0; ot < 4; ++ot)
-    if (ot < NOT)
+  for (int ot = 0; ot < NOT; ++ot)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) redw[lr * GP + ot * 16 + 4 * lq + r] = acc[ot][r];
+    for (int r = 0; r < 4; ++r) redw[lr * GP + ot * 16 + 4 * lq + r] = acc[ot][r] + acs[ot][r];
   __syncthreads();
   float* fp = sd.ws + (int64_t)chain * pl.ws_chain + pl.fp_off[layer] + (int64_t)sl * B * g;
   for (int e = threadIdx.x; e < TR * g; e += blockDim.x) {
@@ -204,7 +243,7 @@ __global__ __launch_bounds__(256) void k_step_fwd(const dgprf_plan_t pl, const S
 }
 
 // ------------------------------------------------------------------------- backward
-template <bool SMALLD>
+template <bool SMALLD, int NOT, bool RBF>
 __global__ __launch_bounds__(256) void k_step_bwd(const dgprf_plan_t pl, const StepDev sd,
                                                   const int layer) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -214,28 +253,42 @@ __global__ __launch_bounds__(256) void k_step_bwd(const dgprf_plan_t pl, const S
   const int L = pl.n_layers;
   const int d = pl.d[layer], R = pl.n_rf[layer], g = pl.n_gp[layer], B = pl.batch;
   const int row0 = rt * TR;
-  const int64_t t = cur_step(sd);
   int64_t* ridx = reinterpret_cast<int64_t*>(smem);
   float* xs = smem + 32;
   float* dfs = smem + LD.aux_off;
   const int dfst = LD.auxst;
   float* red = smem + LD.red_off;
   float* wsc = sd.ws + (int64_t)chain * pl.ws_chain;
+  const float* __restrict__ om = sd.omega + pl.omega_off[layer];
+  const float* __restrict__ W = sd.theta + (int64_t)chain * pl.w_total + pl.w_off[layer];
+  const int cpw = pl.cpw[layer];
+  auto chunk_f0 = [&](int i) { return ((sl * cpw + i) * NW + wave) * 16; };
+  const bool last = layer == L - 1;
 
-  fill_ridx(pl, sd, chain, row0, t, ridx);
-  __syncthreads();
+  float omk[8];
+  if (SMALLD) load_om_frag(om, R, d, chunk_f0(0), lr, lq, omk);
+  const float cl = sd.der[layer];
+
+  if (needs_rows(pl, layer) || last) {
+    fill_ridx(pl, sd, chain, row0, cur_step(sd), ridx);
+    __syncthreads();
+  }
   load_x_tile(pl, sd, layer, chain, row0, ridx, xs, LD.xst);
 
   // dF_l tile [16][g]
-  if (layer == L - 1) {
+  if (last) {
     // likelihood gradient dF = -(1/B) dlogp/dF (likelihoods/gaussian.py:18-25, softmax.py:8-15)
+    const float* fpl = wsc + pl.fp_off[layer];
+    const int64_t ss = (int64_t)B * g;
+    for (int e = threadIdx.x; e < TR * g; e += blockDim.x) {  // F_L = sum of slices
+      const int r = e / g, o = e - r * g, b = row0 + r;
+      dfs[r * dfst + o] = b < B ? sum_slices(fpl + (int64_t)b * g + o, ss) : 0.f;
+    }
+    __syncthreads();
     if (threadIdx.x < TR) {
       const int r = threadIdx.x, b = row0 + r;
       float* df = dfs + r * dfst;
       if (b < B) {
-        const float* fp = wsc + pl.fp_off[layer] + (int64_t)b * g;
-        const int64_t ss = (int64_t)B * g;
-        const int ns = pl.ns[layer];
         const float* y = sd.bd.Y + ridx[r] * sd.bd.y_cols;
         const float invB = 1.0f / (float)B;
         float logp = 0.f;
@@ -243,20 +296,13 @@ __global__ __launch_bounds__(256) void k_step_bwd(const dgprf_plan_t pl, const S
           const float var = sd.der[DGPRF_MAX_LAYERS];
           const float logvar = logf(var);
           for (int o = 0; o < g; ++o) {
-            float f = 0.f;
-            for (int s = 0; s < ns; ++s) f += fp[s * ss + o];
-            const float diff = y[o] - f;
+            const float diff = y[o] - df[o];
             logp += -0.5f * (LOG_2PI + logvar + diff * diff / var);
             df[o] = -(diff / var) * invB;
           }
         } else {
           float mx = -INFINITY;
-          for (int o = 0; o < g; ++o) {
-            float f = 0.f;
-            for (int s = 0; s < ns; ++s) f += fp[s * ss + o];
-            df[o] = f;  // logits staged in place
-            mx = fmaxf(mx, f);
-          }
+          for (int o = 0; o < g; ++o) mx = fmaxf(mx, df[o]);
           float se = 0.f;
           for (int o = 0; o < g; ++o) se += expf(df[o] - mx);
           const float lse = mx + logf(se);
@@ -274,93 +320,67 @@ __global__ __launch_bounds__(256) void k_step_bwd(const dgprf_plan_t pl, const S
     }
   } else {
     // dF_l = dX_{l+1}[:, :g_l] summed over the slices of layer l+1
-    const int nsn = pl.ns[layer + 1];
     const float* dx = wsc + pl.dxp_off[layer + 1];
     const int64_t ss = (int64_t)B * g;
     for (int e = threadIdx.x; e < TR * g; e += blockDim.x) {
       const int r = e / g, o = e - r * g, b = row0 + r;
-      float v = 0.f;
-      if (b < B) {
-        const float* p = dx + (int64_t)b * g + o;
-        for (int s = 0; s < nsn; ++s) v += p[s * ss];
-      }
-      dfs[r * dfst + o] = v;
+      dfs[r * dfst + o] = b < B ? sum_slices(dx + (int64_t)b * g + o, ss) : 0.f;
     }
   }
   __syncthreads();
 
-  const bool rbf = pl.kind[layer] == DGPRF_RBF;
-  const float* __restrict__ om = sd.omega + pl.omega_off[layer];
-  const float* __restrict__ W = sd.theta + (int64_t)chain * pl.w_total + pl.w_off[layer];
-  const float cl = sd.der[layer];
-  const int NOT = (g + 15) >> 4;
   const int KG = (g + 3) >> 2;
   const int dxw = layer > 0 ? pl.n_gp[layer - 1] : 0;
   const int ND = (dxw + 15) >> 4;
 
   float xf[8];
-  if (SMALLD) {
 #pragma unroll
-    for (int ks = 0; ks < 8; ++ks) xf[ks] = (4 * ks < d) ? xs[lr * LD.xst + 4 * ks + lq] : 0.f;
-  }
-  // dF fragments: dff[ks] = dF[row lr][4ks+lq]   (B operand of dPhi, K = g)
+  for (int ks = 0; ks < 8; ++ks) xf[ks] = (SMALLD && 4 * ks < d) ? xs[lr * LD.xst + 4 * ks + lq] : 0.f;
+  // dF fragments: dff[ks] = dF[row lr][4ks+lq]        (B operand of dPhi, K = g)
   //               dfg[ot][r] = dF[row 4lq+r][ot*16+lr] (B operand of gW, K = rows)
-  float dff[16];
+  float dff[4 * NOT];
 #pragma unroll
-  for (int ks = 0; ks < 16; ++ks) {
+  for (int ks = 0; ks < 4 * NOT; ++ks) {
     const int o = 4 * ks + lq;
-    dff[ks] = (ks < KG && o < g) ? dfs[lr * dfst + o] : 0.f;
+    dff[ks] = (o < g) ? dfs[lr * dfst + o] : 0.f;
   }
-  float dfg[4][4];
+  float dfg[NOT][4];
 #pragma unroll
-  for (int ot = 0; ot < 4; ++ot)
+  for (int ot = 0; ot < NOT; ++ot)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int o = ot * 16 + lr;
-      dfg[ot][r] = (ot < NOT && o < g) ? dfs[(4 * lq + r) * dfst + o] : 0.f;
+      dfg[ot][r] = (o < g) ? dfs[(4 * lq + r) * dfst + o] : 0.f;
     }
 
   float* gwp = wsc + pl.gwp_off + (int64_t)rt * pl.w_total + pl.w_off[layer];
   f4 dxa[4] = {f4zero(), f4zero(), f4zero(), f4zero()};
-  const int cpw = pl.cpw[layer];
   for (int i = 0; i < cpw; ++i) {
-    const int f0 = ((sl * cpw + i) * NW + wave) * 16;
+    const int f0 = chunk_f0(i);
     if (f0 >= R) break;
+    if (i > 0 && SMALLD) load_om_frag(om, R, d, f0, lr, lq, omk);
     // ---- gW_l partial over this row tile: rows-in-registers orientation
     {
-      const f4 at = a_tile<SMALLD, true>(om, R, d, f0, xf, xs, LD.xst, lr, lq);
+      const f4 at = a_tile<SMALLD, true>(om, R, d, f0, omk, xf, xs, LD.xst, lr, lq);
       float q0[4], q1[4];
+      features<RBF>(at, cl, q0, q1);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (rbf) {
-          float s, c;
-          rf_sincos(at[r], &s, &c);
-          q0[r] = cl * c;
-          q1[r] = cl * s;
-        } else {
-          q0[r] = cl * fmaxf(at[r], 0.f);
-          q1[r] = 0.f;
+      for (int ot = 0; ot < NOT; ++ot) {
+        f4 gc = f4zero(), gs = f4zero();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          gc = mfma16(q0[r], dfg[ot][r], gc);
+          if (RBF) gs = mfma16(q1[r], dfg[ot][r], gs);
         }
-      }
-#pragma unroll
-      for (int ot = 0; ot < 4; ++ot) {
-        if (ot < NOT) {
-          f4 gc = f4zero(), gs = f4zero();
+        // gc[r] = gW[f0 + 4lq + r][ot*16 + lr]
+        const int o = ot * 16 + lr;
+        if (o < g) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            gc = mfma16(q0[r], dfg[ot][r], gc);
-            if (rbf) gs = mfma16(q1[r], dfg[ot][r], gs);
-          }
-          // gc[r] = gW[f0 + 4lq + r][ot*16 + lr]
-          const int o = ot * 16 + lr;
-          if (o < g) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int f = f0 + 4 * lq + r;
-              if (f < R) {
-                gwp[(int64_t)f * g + o] = gc[r];
-                if (rbf) gwp[(int64_t)(R + f) * g + o] = gs[r];
-              }
+            const int f = f0 + 4 * lq + r;
+            if (f < R) {
+              gwp[(int64_t)f * g + o] = gc[r];
+              if (RBF) gwp[(int64_t)(R + f) * g + o] = gs[r];
             }
           }
         }
@@ -368,17 +388,17 @@ __global__ __launch_bounds__(256) void k_step_bwd(const dgprf_plan_t pl, const S
     }
     if (layer > 0) {
       // ---- dPhi = dF W^T, dA, dX = dA Omega^T : features-in-registers orientation
-      const f4 at = a_tile<SMALLD, false>(om, R, d, f0, xf, xs, LD.xst, lr, lq);
+      const f4 at = a_tile<SMALLD, false>(om, R, d, f0, omk, xf, xs, LD.xst, lr, lq);
       const int fa = f0 + lr;
       f4 dpc = f4zero(), dps = f4zero();
 #pragma unroll
-      for (int ks = 0; ks < 16; ++ks) {
+      for (int ks = 0; ks < 4 * NOT; ++ks) {
         if (ks < KG) {
           const int o = 4 * ks + lq;
           const bool ok = fa < R && o < g;
           const float wc = ok ? W[(int64_t)fa * g + o] : 0.f;
           dpc = mfma16(wc, dff[ks], dpc);
-          if (rbf) {
+          if (RBF) {
             const float wsn = ok ? W[(int64_t)(R + fa) * g + o] : 0.f;
             dps = mfma16(wsn, dff[ks], dps);
           }
@@ -387,7 +407,7 @@ __global__ __launch_bounds__(256) void k_step_bwd(const dgprf_plan_t pl, const S
       float da[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        if (rbf) {
+        if (RBF) {
           float s, c;
           rf_sincos(at[r], &s, &c);
           da[r] = -(cl * s) * dpc[r] + (cl * c) * dps[r];
@@ -461,9 +481,16 @@ __global__ __launch_bounds__(256) void k_step_update(const dgprf_plan_t pl, cons
   if (grad_in) {
     gr = ld4(grad_in + base);
   } else {
+    // sum the row-tile gW partials: groups of 16 independent loads (padding rows are zero)
     const float* gp = sd.ws + (int64_t)chain * pl.ws_chain + pl.gwp_off + e0;
-    f4 s = ld4(gp);
-    for (int rt = 1; rt < pl.n_row_tiles; ++rt) s += ld4(gp + (int64_t)rt * pl.w_total);
+    f4 s = f4zero();
+    for (int rt0 = 0; rt0 < pl.n_rt_pad; rt0 += 16) {
+      f4 v[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v[j] = ld4(gp + (int64_t)(rt0 + j) * pl.w_total);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) s += v[j];
+    }
     // dU/dW = W/N (prior N(0,1), models/dgp.py:129-136,171) + Phi^T dF (likelihood)
     gr = th / N + s;
   }
@@ -507,6 +534,32 @@ __global__ void k_advance(int64_t* step, int64_t by) {
   if (threadIdx.x == 0 && blockIdx.x == 0) *step += by;
 }
 
+#define DGPRF_STEP_LAUNCHER(NAME)                                                                  \
+  template <bool S, int NOT>                                                                       \
+  void NAME##_kind(bool rbf, dim3 grid, size_t lds, hipStream_t s, const dgprf_plan_t& pl,         \
+                   const StepDev& sd, int layer) {                                                 \
+    if (rbf) {                                                                                     \
+      dgprf::set_lds_limit((const void*)k_##NAME<S, NOT, true>, lds);                              \
+      hipLaunchKernelGGL((k_##NAME<S, NOT, true>), grid, dim3(256), lds, s, pl, sd, layer);        \
+    } else {                                                                                       \
+      dgprf::set_lds_limit((const void*)k_##NAME<S, NOT, false>, lds);                             \
+      hipLaunchKernelGGL((k_##NAME<S, NOT, false>), grid, dim3(256), lds, s, pl, sd, layer);       \
+    }                                                                                              \
+  }                                                                                                \
+  template <bool S>                                                                                \
+  void NAME##_not(int NOT, bool rbf, dim3 grid, size_t lds, hipStream_t s, const dgprf_plan_t& pl, \
+                  const StepDev& sd, int layer) {                                                  \
+    switch (NOT) {                                                                                 \
+      case 1: NAME##_kind<S, 1>(rbf, grid, lds, s, pl, sd, layer); break;                          \
+      case 2: NAME##_kind<S, 2>(rbf, grid, lds, s, pl, sd, layer); break;                          \
+      case 3: NAME##_kind<S, 3>(rbf, grid, lds, s, pl, sd, layer); break;                          \
+      default: NAME##_kind<S, 4>(rbf, grid, lds, s, pl, sd, layer); break;                         \
+    }                                                                                              \
+  }
+
+DGPRF_STEP_LAUNCHER(step_fwd)
+DGPRF_STEP_LAUNCHER(step_bwd)
+
 }  // namespace
 
 namespace dgprf {
@@ -517,13 +570,12 @@ hipError_t launch_step_fwd(const dgprf_plan_t& pl, const StepDev& sd, int layer,
   const StepLds LD = step_lds(pl, layer);
   dim3 grid(pl.n_row_tiles, pl.ns[layer], pl.n_chains);
   const size_t lds = (size_t)LD.total * sizeof(float);
-  if (small_d(pl, layer)) {
-    set_lds_limit((const void*)k_step_fwd<true>, lds);
-    hipLaunchKernelGGL(k_step_fwd<true>, grid, dim3(256), lds, s, pl, sd, layer);
-  } else {
-    set_lds_limit((const void*)k_step_fwd<false>, lds);
-    hipLaunchKernelGGL(k_step_fwd<false>, grid, dim3(256), lds, s, pl, sd, layer);
-  }
+  const int NOT = (pl.n_gp[layer] + 15) >> 4;
+  const bool rbf = pl.kind[layer] == DGPRF_RBF;
+  if (small_d(pl, layer))
+    step_fwd_not<true>(NOT, rbf, grid, lds, s, pl, sd, layer);
+  else
+    step_fwd_not<false>(NOT, rbf, grid, lds, s, pl, sd, layer);
   return hipGetLastError();
 }
 
@@ -531,13 +583,12 @@ hipError_t launch_step_bwd(const dgprf_plan_t& pl, const StepDev& sd, int layer,
   const StepLds LD = step_lds(pl, layer);
   dim3 grid(pl.n_row_tiles, pl.ns[layer], pl.n_chains);
   const size_t lds = (size_t)LD.total * sizeof(float);
-  if (small_d(pl, layer)) {
-    set_lds_limit((const void*)k_step_bwd<true>, lds);
-    hipLaunchKernelGGL(k_step_bwd<true>, grid, dim3(256), lds, s, pl, sd, layer);
-  } else {
-    set_lds_limit((const void*)k_step_bwd<false>, lds);
-    hipLaunchKernelGGL(k_step_bwd<false>, grid, dim3(256), lds, s, pl, sd, layer);
-  }
+  const int NOT = (pl.n_gp[layer] + 15) >> 4;
+  const bool rbf = pl.kind[layer] == DGPRF_RBF;
+  if (small_d(pl, layer))
+    step_bwd_not<true>(NOT, rbf, grid, lds, s, pl, sd, layer);
+  else
+    step_bwd_not<false>(NOT, rbf, grid, lds, s, pl, sd, layer);
   return hipGetLastError();
 }
 

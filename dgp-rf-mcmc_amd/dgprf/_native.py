@@ -38,7 +38,7 @@ class Plan(ctypes.Structure):
         ("kind", _i32 * _L), ("n_rf", _i32 * _L), ("n_gp", _i32 * _L),
         ("initialised", _i32),
         ("d", _i32 * _L), ("P", _i32 * _L), ("ns", _i32 * _L), ("cpw", _i32 * _L),
-        ("n_row_tiles", _i32), ("pad0", _i32),
+        ("n_row_tiles", _i32), ("n_rt_pad", _i32),
         ("omega_off", _i64 * _L), ("w_off", _i64 * _L), ("lis_off", _i64 * _L),
         ("mean_off", _i64 * _L), ("fp_off", _i64 * _L), ("dxp_off", _i64 * _L),
         ("gwp_off", _i64), ("logp_off", _i64),

@@ -97,14 +97,14 @@ typedef struct dgprf_plan {
   int32_t ns[DGPRF_MAX_LAYERS];     /* feature slices per step kernel */
   int32_t cpw[DGPRF_MAX_LAYERS];    /* 16-feature chunks per wave per slice */
   int32_t n_row_tiles;              /* ceil(B/16) */
-  int32_t pad0;
+  int32_t n_rt_pad;                 /* n_row_tiles rounded up to 16 (zero rows in gW partials) */
   int64_t omega_off[DGPRF_MAX_LAYERS];
   int64_t w_off[DGPRF_MAX_LAYERS];
   int64_t lis_off[DGPRF_MAX_LAYERS];
   int64_t mean_off[DGPRF_MAX_LAYERS];
-  int64_t fp_off[DGPRF_MAX_LAYERS];  /* F partials  [ns][B][g]      (per chain) */
-  int64_t dxp_off[DGPRF_MAX_LAYERS]; /* dX partials [ns][B][g_{l-1}] (per chain, l>=1) */
-  int64_t gwp_off;                   /* gW partials [n_row_tiles][w_total] (per chain) */
+  int64_t fp_off[DGPRF_MAX_LAYERS];  /* F partials  [16][B][g] (per chain; slices >= ns stay 0) */
+  int64_t dxp_off[DGPRF_MAX_LAYERS]; /* dX partials [16][B][g_{l-1}] (per chain, l>=1)      */
+  int64_t gwp_off;                   /* gW partials [n_rt_pad][w_total] (per chain)           */
   int64_t logp_off;                  /* per-row minibatch log p [B] (per chain) */
   int64_t omega_total;
   int64_t w_total;
@@ -204,10 +204,10 @@ int dgprf_graph_create_sghmc(dgprf_graph_handle *out, const dgprf_plan_t *plan,
 int dgprf_graph_launch(dgprf_graph_handle graph, void *stream);
 int dgprf_graph_destroy(dgprf_graph_handle graph);
 
-/* Per-kernel device time of one step, measured with hipEvents on `stream`: each of the 2L+1 step
- * kernels (forward l = 0..L-1, backward l = 0..L-1, update) is launched `reps` times back to back
- * and ms_out[k] receives its average milliseconds per launch.  Runs one full step first so the
- * workspaces hold live data; advances the chain (the update kernel runs reps + 1 times). */
+/* Per-kernel device time of the step sequence, measured with hipEvents on `stream`: `reps` real
+ * steps (forward l = 0..L-1, backward L-1..0, update; the chain advances) with an event pair around
+ * every kernel.  ms_out[k] receives the mean milliseconds of kernel k, indexed forward l -> l,
+ * backward l -> L + l, update -> 2L. */
 int dgprf_profile_step(const dgprf_plan_t *plan, const dgprf_chain_t *chain,
                        const dgprf_batch_t *batch, const dgprf_step_t *step, int32_t reps,
                        float *ms_out, void *stream);
