@@ -94,14 +94,17 @@ int check_step(const dgprf_step_t* st) {
   return DGPRF_OK;
 }
 
-// fwd for every layer, bwd in reverse, then the fused update (or gradient reduction).
+// [gather rows] fwd for every layer, bwd in reverse, then the fused update (or gradient
+// reduction).  prep_gather: gather this step's minibatch rows first; gather_next: the update
+// kernel gathers step t+1's rows (graph replays, where the next step is known to follow).
 hipError_t enqueue_step(const dgprf_plan_t& pl, const StepDev& sd, const UpdateDev& ud,
-                        hipStream_t s) {
+                        hipStream_t s, bool prep_gather = true, bool gather_next = false) {
   hipError_t e = hipSuccess;
+  if (prep_gather) e = dgprf::launch_gather(pl, sd, s);
   for (int l = 0; l < pl.n_layers && e == hipSuccess; ++l) e = dgprf::launch_step_fwd(pl, sd, l, s);
   for (int l = pl.n_layers - 1; l >= 0 && e == hipSuccess; --l)
     e = dgprf::launch_step_bwd(pl, sd, l, s);
-  if (e == hipSuccess) e = dgprf::launch_step_update(pl, sd, ud, nullptr, s);
+  if (e == hipSuccess) e = dgprf::launch_step_update(pl, sd, ud, nullptr, s, gather_next);
   return e;
 }
 
@@ -199,6 +202,12 @@ int dgprf_plan_init(dgprf_plan_t* pl) {
   ws = align4(ws + (int64_t)pl->n_rt_pad * pl->w_total);
   pl->logp_off = ws;
   ws = align4(ws + B);
+  pl->yb_cols = pl->likelihood == DGPRF_LIK_SOFTMAX ? 1 : pl->n_gp[L - 1];
+  pl->xb_off = ws;
+  ws = align4(ws + (int64_t)B * pl->d_in);
+  pl->yb_off = ws;
+  ws = align4(ws + (int64_t)B * pl->yb_cols);
+  pl->pad2 = 0;
   pl->ws_chain = ws;
   pl->ws_total = ws * pl->n_chains;
   pl->initialised = 1;
@@ -271,7 +280,7 @@ int dgprf_graph_create_sghmc(dgprf_graph_handle* out, const dgprf_plan_t* plan,
   const UpdateDev ud = make_update_dev(st);
   for (int k = 0; k < steps_per_graph && e == hipSuccess; ++k) {
     const StepDev sd = make_step_dev(*plan, *chain, *batch, st.step_offset + k);
-    e = enqueue_step(*plan, sd, ud, cs);
+    e = enqueue_step(*plan, sd, ud, cs, k == 0, k + 1 < steps_per_graph);
   }
   if (e == hipSuccess) e = dgprf::launch_advance(chain->step, steps_per_graph, cs);
   hipGraph_t g = nullptr;
@@ -330,6 +339,7 @@ int dgprf_profile_step(const dgprf_plan_t* plan, const dgprf_chain_t* chain,
   // the real step sequence (fwd 0..L-1, bwd L-1..0, update), every kernel between two events
   for (int rep = 0; rep < reps && e == hipSuccess; ++rep) {
     const StepDev sd = make_step_dev(*plan, *chain, *batch, st.step_offset);
+    e = dgprf::launch_gather(*plan, sd, s);
     for (int j = 0; j < K && e == hipSuccess; ++j) {
       const int kk = j < L ? j : (j < 2 * L ? L + (2 * L - 1 - j) : 2 * L);
       e = hipEventRecord(ev[2 * kk], s);

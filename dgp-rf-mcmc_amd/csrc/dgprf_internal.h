@@ -27,6 +27,32 @@ struct UpdateDev {
   const float* xi_resample;
 };
 
+// In-kernel timestamps for a separate diagnostic build (-DDGPRF_STAMPS); never in the product.
+#ifdef DGPRF_STAMPS
+extern __device__ unsigned long long g_dgprf_stamps[];
+#define DGPRF_STAMP_SLOTS 16
+#define DGPRF_STAMP(base, i)                                                      \
+  do {                                                                           \
+    if (threadIdx.x == 0) {                                                      \
+      __builtin_amdgcn_sched_barrier(0);                                         \
+      g_dgprf_stamps[(size_t)(base) * DGPRF_STAMP_SLOTS + (i)] =                 \
+          __builtin_amdgcn_s_memtime();                                          \
+      if ((i) == 0)                                                              \
+        g_dgprf_stamps[(size_t)(base) * DGPRF_STAMP_SLOTS + 15] =                \
+            __builtin_amdgcn_s_memrealtime();                                    \
+      if ((i) == 14)                                                             \
+        g_dgprf_stamps[(size_t)(base) * DGPRF_STAMP_SLOTS + 13] =                \
+            __builtin_amdgcn_s_memrealtime();                                    \
+      __builtin_amdgcn_sched_barrier(0);                                         \
+    }                                                                            \
+  } while (0)
+#else
+#define DGPRF_STAMP(base, i) \
+  do {                       \
+    (void)(base);            \
+  } while (0)
+#endif
+
 namespace dgprf {
 // Dynamic LDS above 64 KiB must be opted into per kernel.
 inline void set_lds_limit(const void* fn, size_t bytes) {
@@ -36,7 +62,9 @@ inline void set_lds_limit(const void* fn, size_t bytes) {
 hipError_t launch_step_fwd(const dgprf_plan_t& pl, const StepDev& sd, int layer, hipStream_t s);
 hipError_t launch_step_bwd(const dgprf_plan_t& pl, const StepDev& sd, int layer, hipStream_t s);
 hipError_t launch_step_update(const dgprf_plan_t& pl, const StepDev& sd, const UpdateDev& ud,
-                              const float* grad_in, hipStream_t s);
+                              const float* grad_in, hipStream_t s, bool gather_next = false);
+// minibatch rows of step *step + step_offset into the workspace (no-op for DGPRF_BATCH_DIRECT)
+hipError_t launch_gather(const dgprf_plan_t& pl, const StepDev& sd, hipStream_t s);
 hipError_t launch_advance(int64_t* step, int64_t by, hipStream_t s);
 
 hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const float* omega,

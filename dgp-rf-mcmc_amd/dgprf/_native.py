@@ -43,7 +43,8 @@ class Plan(ctypes.Structure):
         ("mean_off", _i64 * _L), ("fp_off", _i64 * _L), ("dxp_off", _i64 * _L),
         ("gwp_off", _i64), ("logp_off", _i64),
         ("omega_total", _i64), ("w_total", _i64), ("hyp_total", _i64), ("der_total", _i64),
-        ("ws_chain", _i64), ("ws_total", _i64),
+        ("ws_chain", _i64), ("ws_total", _i64), ("xb_off", _i64), ("yb_off", _i64),
+        ("yb_cols", _i32), ("pad2", _i32),
     ]
 
 

@@ -112,6 +112,10 @@ typedef struct dgprf_plan {
   int64_t der_total;
   int64_t ws_chain;
   int64_t ws_total;
+  int64_t xb_off;                    /* gathered minibatch rows X [B][d_in] (per chain)        */
+  int64_t yb_off;                    /* gathered minibatch targets [B][yb_cols] (per chain)    */
+  int32_t yb_cols;                   /* g_L (Gaussian) or 1 (softmax label)                    */
+  int32_t pad2;
 } dgprf_plan_t;
 
 /* Device state of the chains.  Replaces the tf.Variables W and their ad-hoc attributes

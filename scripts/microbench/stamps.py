@@ -1,0 +1,65 @@
+"""Diagnostic: per-segment cycle counts of the step kernels from the -DDGPRF_STAMPS build.
+
+  make -C dgp-rf-mcmc_amd/csrc OUT=../../scripts/microbench/libdgprf_stamps.so EXTRA=-DDGPRF_STAMPS
+  DGPRF_LIB=scripts/microbench/libdgprf_stamps.so python scripts/microbench/stamps.py
+Stamps are read only from their own buffer; nothing here is a product number (stamps serialise).
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "dgp-rf-mcmc_amd")]
+
+from dgprf import _native as N  # noqa: E402
+from dgprf import engine as E  # noqa: E402
+from dgprf.data import regression_data  # noqa: E402
+from likelihoods import Gaussian  # noqa: E402
+from models.regression_model import RegressionDGP  # noqa: E402
+
+SLOTS = 16
+dev = torch.device("cuda", 0)
+X, Y, _ = regression_data(1_000_000, 8, 0, device=dev)
+m = RegressionDGP(8, 1, n_hidden_layers=3, n_rf=1024, n_gp=[8, 8, 1], likelihood=Gaussian())
+m.precond_update(None, 1_000_000, precond_type="identity")
+eng = m._engine
+lib = N.lib()
+for _ in range(50):
+    eng.step(X, Y, 1_000_000, 0.01, 0.9, 1.0, batch_size=200, mode=2)
+torch.cuda.synchronize()
+lib.dgprf_debug_clear_stamps()
+for _ in range(3):
+    eng.step(X, Y, 1_000_000, 0.01, 0.9, 1.0, batch_size=200, mode=2)
+torch.cuda.synchronize()
+n = 17 * 4096 * SLOTS
+buf = (ctypes.c_ulonglong * n)()
+assert lib.dgprf_debug_read_stamps(buf, n) == 0
+S = np.frombuffer(buf, dtype=np.uint64).reshape(17, 4096, SLOTS).astype(np.int64)
+names = {0: "fwd0", 2: "fwd1", 4: "fwd2", 1: "bwd0", 3: "bwd1", 5: "bwd2", 16: "update"}
+order = [0, 2, 4, 5, 3, 1, 16]
+t0_all = []
+for k in order:
+    st = S[k]
+    valid = st[:, 0] > 0
+    st = st[valid]
+    if len(st) == 0:
+        continue
+    real0, real_end = st[:, 15], st[:, 13]
+    cyc = st[:, 14] - st[:, 0]
+    freq = cyc / np.maximum(real_end - real0, 1) * 100e6
+    segs = []
+    marks = [i for i in range(0, 15) if (st[:, i] > 0).all()]
+    for a, b in zip(marks[:-1], marks[1:]):
+        segs.append(f"{a}->{b}: {np.median(st[:, b] - st[:, a]):.0f}")
+    span = (real_end.max() - real0.min()) * 10
+    skew = (real0.max() - real0.min()) * 10
+    print(f"{names[k]:7s} WGs={len(st):4d} clock~{np.median(freq) / 1e9:.2f}GHz  "
+          f"median cycles [{', '.join(segs)}]  total {np.median(cyc):.0f}  "
+          f"span {span:.0f} ns  start-skew {skew:.0f} ns")
+    t0_all.append((names[k], real0.min(), real_end.max()))
+print("kernel-to-kernel (first WG start of next - last WG end of previous), ns:")
+for (a, s0, e0), (b, s1, e1) in zip(t0_all[:-1], t0_all[1:]):
+    print(f"  {a} -> {b}: {(s1 - e0) * 10}")
