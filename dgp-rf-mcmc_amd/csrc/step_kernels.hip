@@ -69,7 +69,7 @@ struct UpdK {
   uint64_t seed;
   int64_t w_total, ws_cs;
   int64_t lo[DGPRF_MAX_LAYERS], hi[DGPRF_MAX_LAYERS];
-  int32_t n_rt_pad, n_layers, step_offset, pad;
+  int32_t n_rt_pad, n_layers, step_offset, upd_blocks;
   UpdateDev ud;
   // gather of step t+1's minibatch rows (graph mode)
   int32_t gather_next, B, d_in, yb_cols;
@@ -93,7 +93,7 @@ __host__ __device__ inline void step_lds(int d, int g, LayerK& a, int& total) {
   a.xst = round4(d) + 1;
   a.aux_off = round4(TR * a.xst);
   a.auxst = g + 1;
-  a.red_off = a.aux_off + round4(TR * a.auxst);
+  a.red_off = a.aux_off + 2 * round4(TR * a.auxst);  // dF tile + Y tile
   total = a.red_off + NW * TR * 64;
 }
 
@@ -338,17 +338,22 @@ __global__ __launch_bounds__(256) void k_step_bwd(const LayerK a) {
   if (a.last) {
     // likelihood gradient dF = -(1/B) dlogp/dF (likelihoods/gaussian.py:18-25, softmax.py:8-15)
     const float* fpl = a.fout + (int64_t)chain * a.ws_cs;
-    for (int e = threadIdx.x; e < TR * g; e += blockDim.x) {  // F_L = sum of slices
-      const int r = e / g, o = e - r * g, b = row0 + r;
-      const float v = sum_slices(fpl + (int64_t)min(b, B - 1) * g + o, (int64_t)B * g);
+    const float* yr = a.yrows + (int64_t)chain * a.yrow_cs;
+    float* ysh = dfs + round4(TR * dfst);
+    const int yc = a.likelihood == DGPRF_LIK_GAUSSIAN ? g : 1;
+    for (int e = threadIdx.x; e < TR * g; e += blockDim.x) {  // F_L = sum of slices; Y alongside
+      const int r = e / g, o = e - r * g, b = row0 + r, bc = min(b, B - 1);
+      const float v = sum_slices(fpl + (int64_t)bc * g + o, (int64_t)B * g);
+      const float yv = yr[(int64_t)bc * a.y_cols + min(o, yc - 1)];
       dfs[r * dfst + o] = b < B ? v : 0.f;
+      ysh[r * dfst + o] = yv;
     }
     __syncthreads();
     if (threadIdx.x < TR) {
       const int r = threadIdx.x, b = row0 + r;
       float* df = dfs + r * dfst;
       if (b < B) {
-        const float* y = a.yrows + (int64_t)chain * a.yrow_cs + (int64_t)b * a.y_cols;
+        const float* y = ysh + r * dfst;
         const float invB = 1.0f / (float)B;
         float logp = 0.f;
         if (a.likelihood == DGPRF_LIK_GAUSSIAN) {
@@ -550,9 +555,13 @@ __global__ __launch_bounds__(256) void k_step_update(const UpdK a) {
   DGPRF_STAMP(stamp_base, 0);
   const UpdateDev& ud = a.ud;
   const int64_t t = *a.step + (int64_t)a.step_offset;
-  if (a.gather_next && q < a.B)  // rows of step t+1 (off the next forward's critical path)
-    gather_row(a.bd, a.B, a.d_in, a.yb_cols, a.xb + (int64_t)chain * a.ws_cs,
-               a.yb + (int64_t)chain * a.ws_cs, chain, t + 1, (int)q);
+  if ((int)blockIdx.x >= a.upd_blocks) {  // dedicated blocks: rows of step t+1 (off the path)
+    const int b = ((int)blockIdx.x - a.upd_blocks) * blockDim.x + threadIdx.x;
+    if (a.gather_next && b < a.B)
+      gather_row(a.bd, a.B, a.d_in, a.yb_cols, a.xb + (int64_t)chain * a.ws_cs,
+                 a.yb + (int64_t)chain * a.ws_cs, chain, t + 1, b);
+    return;
+  }
   if (e0 >= a.w_total) return;
   int layer = -1;
 #pragma unroll
@@ -748,7 +757,6 @@ hipError_t launch_step_update(const dgprf_plan_t& pl, const StepDev& sd, const U
   a.n_rt_pad = pl.n_rt_pad;
   a.n_layers = pl.n_layers;
   a.step_offset = sd.step_offset;
-  a.pad = 0;
   a.ud = ud;
   a.gather_next = gather_next && sd.bd.mode == DGPRF_BATCH_EPOCH ? 1 : 0;
   a.B = pl.batch;
@@ -758,8 +766,8 @@ hipError_t launch_step_update(const dgprf_plan_t& pl, const StepDev& sd, const U
   a.xb = sd.ws ? sd.ws + pl.xb_off : nullptr;
   a.yb = sd.ws ? sd.ws + pl.yb_off : nullptr;
   const int64_t quads = pl.w_total / 4;
-  int64_t blocks = (quads + 255) / 256;
-  if (a.gather_next) blocks = blocks > (pl.batch + 255) / 256 ? blocks : (pl.batch + 255) / 256;
+  a.upd_blocks = (int)((quads + 255) / 256);
+  const int64_t blocks = a.upd_blocks + (a.gather_next ? (pl.batch + 255) / 256 : 0);
   dim3 grid((unsigned)blocks, pl.n_chains);
   hipLaunchKernelGGL(k_step_update, grid, dim3(256), 0, s, a);
   return hipGetLastError();
