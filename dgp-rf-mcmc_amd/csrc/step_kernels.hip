@@ -34,6 +34,7 @@ constexpr int NW = DGPRF_WAVES;
 constexpr int TR = DGPRF_TILE_ROWS;
 constexpr int NSM = DGPRF_NS_MAX;
 constexpr float LOG_2PI = 1.8378770664093453f;
+constexpr int OST = 68;  // LDS row stride of the staged Omega block (16B-aligned rows)
 
 __host__ __device__ __forceinline__ int round4(int x) { return (x + 3) & ~3; }
 
@@ -55,6 +56,10 @@ struct LayerK {
   int32_t d, R, g, gp, dxw, cpw, B, d_in, y_cols;
   int32_t last, likelihood, layer;
   int32_t xst, aux_off, auxst, red_off;
+  int32_t stg_off, os_off;       // backward operand staging: W rows [2][64*g], Omega rows [.][OST]
+  // element-owner prologue (fast == 1): workspace offsets of the partial buffers, magic divisors
+  const float* ws;      // chain 0 workspace (chain stride ws_cs)
+  int32_t fast, fprev_off, dsrc_off, xmag, dmag;
 };
 
 // Arguments of the update kernel.
@@ -78,6 +83,10 @@ struct UpdK {
   float* yb;
 };
 
+// v if ok else 0, written so that the compiler cannot sink the (always in-range, finite) load
+// into an exec-masked branch followed by an immediate wait: the load result is used on every path.
+__device__ __forceinline__ float keep(float v, bool ok) { return v * (ok ? 1.f : 0.f); }
+
 // sum over the DGPRF_NS_MAX slices of a partial buffer: independent loads, fixed order.
 __device__ __forceinline__ float sum_slices(const float* __restrict__ p, int64_t stride) {
   float v[NSM];
@@ -94,7 +103,29 @@ __host__ __device__ inline void step_lds(int d, int g, LayerK& a, int& total) {
   a.aux_off = round4(TR * a.xst);
   a.auxst = g + 1;
   a.red_off = a.aux_off + 2 * round4(TR * a.auxst);  // dF tile + Y tile
-  total = a.red_off + NW * TR * 64;
+  // backward: the workgroup's 64-feature block of W_l ([2][64*g] raw) and Omega_l ([64][OST])
+  a.stg_off = a.red_off + NW * TR * 64;
+  a.os_off = a.stg_off + (2 * 64 * g > 2048 ? round4(2 * 64 * g) : 2048);
+  total = a.os_off + 64 * OST;
+}
+
+// floor(i / n) = (i * magic(n)) >> 20 for 0 <= i < 4096, 1 <= n <= 256
+__host__ __device__ inline int div_magic(int n) { return (int)((1048576 + n - 1) / n); }
+
+// ---- single-burst prologue: every operand tile of a workgroup is fetched with one
+// buffer_load_dwordx4 per 16 bytes (no redundant lanes; lanes past a tile get an out-of-range
+// offset, which returns 0 without a memory access), all loads issued before the first wait.
+constexpr uint32_t OOB = 0x80000000u;
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+__device__ __forceinline__ rsrc_t make_rsrc(const float* p, int64_t n_floats) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)(n_floats * 4), 0x00020000);
+}
+__device__ __forceinline__ f4 bload4(rsrc_t r, uint32_t byte_off) {
+  return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
+}
+__device__ __forceinline__ float bload1(rsrc_t r, uint32_t byte_off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
 }
 
 // X_l[16][d] of batch rows row0..: F_{l-1} partial sums (+ [F | X] dataset columns for input_cat,
@@ -115,6 +146,74 @@ __device__ __forceinline__ void load_x_tile(const LayerK& a, int chain, int row0
   }
 }
 
+// ---- element-owner prologue (a.fast == 1).  Thread t owns tile elements u = t + 256p (p < 2):
+// the X tile (TR x dpad: F_{l-1} slice partials | dataset columns) first, then, in the backward,
+// the dF tile (TR x g: dX_{l+1} or F_L slice partials, with the matching Y value).  Every owned
+// element issues its 16 slice loads on the chain's workspace plus one dataset / Y load; absent
+// slices, rows >= B and padding columns get an out-of-range offset (0, no memory access).  All
+// loads of the prologue are issued before the first sum, which runs in registers in the same fixed
+// slice order as sum_slices.
+struct Elem {
+  float v[NSM];
+  float xd, y;
+  int dst;  // LDS index (xs / dfs), or -1
+  bool isx;
+};
+
+__device__ __forceinline__ void elem_issue(const LayerK& a, int chain, int row0, int u,
+                                           int nd_tile, int dfst, Elem& e) {
+  const rsrc_t rws = make_rsrc(a.ws + (int64_t)chain * a.ws_cs, a.ws_cs);
+  const rsrc_t rx = make_rsrc(a.xrows + (int64_t)chain * a.xrow_cs, (int64_t)a.B * (a.d - a.gp));
+  const rsrc_t ry = make_rsrc(a.yrows + (int64_t)chain * a.yrow_cs, (int64_t)a.B * a.y_cols);
+  const int dpad = round4(a.d), nx = TR * dpad, ndat = a.d - a.gp;
+  const bool isx = u < nx, isd = !isx && u < nx + nd_tile;
+  const int ud = u - nx;
+  const int r = isx ? (u * a.xmag) >> 20 : (ud * a.dmag) >> 20;
+  const int c = isx ? u - r * dpad : ud - r * a.g;
+  const int b = row0 + r;
+  const bool inb = b < a.B && (isx || isd);
+  const bool fromp = inb && (isx ? c < a.gp : true);
+  const int w = isx ? a.gp : a.g;
+  const int base = (isx ? a.fprev_off : a.dsrc_off) + b * w + c;
+  const int str = a.B * w;
+#pragma unroll
+  for (int sl = 0; sl < NSM; ++sl)
+    e.v[sl] = bload1(rws, fromp ? (uint32_t)((base + sl * str) * 4) : OOB);
+  const bool xdat = inb && isx && c >= a.gp && c < a.d;
+  e.xd = bload1(rx, xdat ? (uint32_t)((b * ndat + (c - a.gp)) * 4) : OOB);
+  const int yc = a.likelihood == DGPRF_LIK_GAUSSIAN ? a.g : 1;
+  const bool ydat = inb && isd && a.last;
+  e.y = bload1(ry, ydat ? (uint32_t)((b * a.y_cols + min(c, yc - 1)) * 4) : OOB);
+  e.isx = isx;
+  e.dst = isx ? r * a.xst + c : (isd ? r * dfst + c : -1);
+}
+// sum + store: xs[dst] or dfs[dst] (and ysh[dst]); non-owning lanes write a scratch slot
+__device__ __forceinline__ void elem_store(const Elem& e, float* xs, float* dfs, float* ysh,
+                                          float* scratch) {
+  float acc = e.v[0];
+#pragma unroll
+  for (int sl = 1; sl < NSM; ++sl) acc += e.v[sl];
+  const float val = e.isx ? acc + e.xd : acc;  // exactly one of the two is non-zero-sourced
+  float* dv = e.dst < 0 ? scratch : (e.isx ? xs + e.dst : dfs + e.dst);
+  float* dy = (e.dst < 0 || e.isx) ? scratch + 256 : ysh + e.dst;
+  *dv = val;
+  *dy = e.y;
+}
+
+// Element-owner prologue of one kernel: X tile (and dF tile when nd_tile > 0) into LDS.
+__device__ __forceinline__ void elem_prologue(const LayerK& a, int chain, int row0, int nd_tile,
+                                             float* xs, float* dfs, int dfst, float* ysh,
+                                             float* scratch) {
+  const int total = TR * round4(a.d) + nd_tile;
+  const int t = threadIdx.x;
+  const int wave0 = __builtin_amdgcn_readfirstlane(t & ~63);
+  Elem e0, e1;
+  if (wave0 < total) elem_issue(a, chain, row0, t, nd_tile, dfst, e0);
+  if (256 + wave0 < total) elem_issue(a, chain, row0, t + 256, nd_tile, dfst, e1);
+  if (wave0 < total) elem_store(e0, xs, dfs, ysh, scratch + t);
+  if (256 + wave0 < total) elem_store(e1, xs, dfs, ysh, scratch + t);
+}
+
 // Omega fragments: omk[ks] = Omega[4ks+lq][f0+lr] (zero outside the layer), KS k-steps.
 template <int KS>
 __device__ __forceinline__ void load_om_frag(const float* __restrict__ om, int R, int d, int f0,
@@ -124,8 +223,7 @@ __device__ __forceinline__ void load_om_frag(const float* __restrict__ om, int R
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
     const int k = 4 * ks + lq;
-    const float v = om[(int64_t)min(k, d - 1) * R + fc];
-    omk[ks] = (fa < R && k < d) ? v : 0.f;
+    omk[ks] = keep(om[(int64_t)min(k, d - 1) * R + fc], fa < R && k < d);
   }
 }
 
@@ -187,11 +285,9 @@ __device__ __forceinline__ void load_w_frag(const float* __restrict__ W, int R, 
     for (int r = 0; r < 4; ++r) {
       const int fr = f0 + 4 * lq + r, fc = min(fr, R - 1);
       const bool ok = o < g && fr < R;
-      const float v0 = W[(int64_t)fc * g + oc];
-      wf[ot][r][0] = ok ? v0 : 0.f;
+      wf[ot][r][0] = keep(W[(int64_t)fc * g + oc], ok);
       if (RBF) {
-        const float v1 = W[(int64_t)(R + fc) * g + oc];
-        wf[ot][r][1] = ok ? v1 : 0.f;
+        wf[ot][r][1] = keep(W[(int64_t)(R + fc) * g + oc], ok);
       } else {
         wf[ot][r][1] = 0.f;
       }
@@ -220,7 +316,11 @@ __global__ __launch_bounds__(256) void k_step_fwd(const LayerK a) {
   load_w_frag<NOT, RBF>(W, R, g, chunk_f0(0), lr, lq, wf);
   const float cl = *a.cptr;
   DGPRF_STAMP(stamp_base, 1);
-  load_x_tile(a, chain, row0, xs);
+  if (a.fast) {
+    elem_prologue(a, chain, row0, 0, xs, red, 0, red, red);  // no dF tile: unused targets
+  } else {
+    load_x_tile(a, chain, row0, xs);
+  }
   __syncthreads();
   DGPRF_STAMP(stamp_base, 2);
 
@@ -304,50 +404,87 @@ __global__ __launch_bounds__(256) void k_step_bwd(const LayerK a) {
   // first chunk's fragments, issued before the dependent partial sums
   float omk[8];
   if (KS > 0) load_om_frag<KS>(a.om, R, d, chunk_f0(0), lr, lq, omk);
-  float wdp[KGM][2];  // dPhi A operand: W[f0+lr (| R+...)][4ks+lq]
-  float omx[4][4];    // dX A operand: Omega[dt*16+lr][f0+4lq+r]
-  auto load_bwd_frag = [&](int f0) {
-    const int fa = f0 + lr, fc = min(fa, R - 1);
+  // dPhi / dX A operands (W_l rows and Omega_l rows of this workgroup's 64-feature block) are
+  // staged through LDS as W [2][64*g] (raw rows) and Omega [rows][OST]; the fragment reads zero
+  // feature rows >= R.
+  float* wsl = smem + a.stg_off;
+  float* osl = smem + a.os_off;
+  const int nwh = 64 * g, nwt = RBF ? 2 * nwh : nwh, nom = dxw * 64;
+  // general path: clamped scalar loads (contiguous runs), used when a.fast == 0 and for cpw > 1
+  constexpr int NJW = 8 * NOT;  // >= 2*64*g/256
+  constexpr int NJO = 16;       // >= 64*64/256
+  float stw[NJW], sto[NJO];
+  auto stage_load = [&](int fb) {
+    const int64_t rg = (int64_t)R * g;
 #pragma unroll
-    for (int ks = 0; ks < KGM; ++ks) {
-      const int o = 4 * ks + lq, oc = min(o, g - 1);
-      const bool ok = fa < R && o < g;
-      const float v0 = W[(int64_t)fc * g + oc];
-      wdp[ks][0] = ok ? v0 : 0.f;
-      if (RBF) {
-        const float v1 = W[(int64_t)(R + fc) * g + oc];
-        wdp[ks][1] = ok ? v1 : 0.f;
-      } else {
-        wdp[ks][1] = 0.f;
-      }
+    for (int j = 0; j < NJW; ++j) {
+      const int e = min((int)threadIdx.x + 256 * j, nwt - 1);
+      const int h = e >= nwh, e2 = e - h * nwh;
+      stw[j] = W[h * rg + min((int64_t)fb * g + e2, rg - 1)];
     }
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int k = dt * 16 + lr, f = f0 + 4 * lq + r;
-        const float v = om_safe(a.om, R, max(dxw, 1), k, f);
-        omx[dt][r] = (k < dxw && f < R) ? v : 0.f;
-      }
+    for (int j = 0; j < NJO; ++j) {
+      const int e = min((int)threadIdx.x + 256 * j, nom - 1);
+      sto[j] = a.om[(int64_t)(e >> 6) * R + min(fb + (e & 63), R - 1)];
+    }
   };
-  if (dxw > 0) load_bwd_frag(chunk_f0(0));
+  auto stage_store = [&](int fb) {
+#pragma unroll
+    for (int j = 0; j < NJW; ++j) {
+      const int e = (int)threadIdx.x + 256 * j;
+      if (e < nwt) wsl[e] = stw[j];
+    }
+#pragma unroll
+    for (int j = 0; j < NJO; ++j) {
+      const int e = (int)threadIdx.x + 256 * j;
+      if (e < nom) osl[(e >> 6) * OST + (e & 63)] = fb + (e & 63) < R ? sto[j] : 0.f;
+    }
+  };
+  const int fb0 = (sl * cpw) * 64;
   const float cl = *a.cptr;
-  load_x_tile(a, chain, row0, xs);
+  const float* fpl = a.fout + (int64_t)chain * a.ws_cs;        // F_L partials (last layer)
+  const float* dxn = a.dxnext + (int64_t)chain * a.ws_cs;      // dX_{l+1} partials
+  const float* yr = a.yrows + (int64_t)chain * a.yrow_cs;
+  float* ysh = dfs + round4(TR * dfst);
+  const int yc = a.likelihood == DGPRF_LIK_GAUSSIAN ? g : 1;
+  if (a.fast) {
+    // ---- single burst: W/Omega block, X tile, dF (or F_L) partials and Y rows
+    f4 sw[2], so;
+    if (dxw > 0) {
+      const rsrc_t rw = make_rsrc(W, (int64_t)(RBF ? 2 : 1) * R * g);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int i = (int)threadIdx.x + 256 * j, h = i >= 16 * g, q = i - h * 16 * g;
+        const uint32_t off = (uint32_t)((((h * R) + fb0) * g + 4 * q) * 4);
+        sw[j] = bload4(rw, i < (RBF ? 32 : 16) * g ? off : OOB);
+      }
+      const rsrc_t ro = make_rsrc(a.om, (int64_t)dxw * R);
+      const int k = threadIdx.x >> 4, c4 = threadIdx.x & 15;
+      so = bload4(ro, k < dxw && fb0 + 4 * c4 < R ? (uint32_t)((k * R + fb0 + 4 * c4) * 4) : OOB);
+    }
+    DGPRF_STAMP(stamp_base, 1);
+    elem_prologue(a, chain, row0, TR * g, xs, dfs, dfst, ysh, red);
+    if (dxw > 0) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) *reinterpret_cast<f4*>(wsl + 4 * ((int)threadIdx.x + 256 * j)) = sw[j];
+      *reinterpret_cast<f4*>(osl + (threadIdx.x >> 4) * OST + 4 * (threadIdx.x & 15)) = so;
+    }
+    DGPRF_STAMP(stamp_base, 4);
+  } else {
+    if (dxw > 0) stage_load(fb0);
+    load_x_tile(a, chain, row0, xs);
+    for (int e = threadIdx.x; e < TR * g; e += blockDim.x) {  // dF (or F_L) slice sums; Y alongside
+      const int r = e / g, o = e - r * g, b = row0 + r, bc = min(b, B - 1);
+      const float v = sum_slices((a.last ? fpl : dxn) + (int64_t)bc * g + o, (int64_t)B * g);
+      dfs[r * dfst + o] = b < B ? v : 0.f;
+      if (a.last) ysh[r * dfst + o] = yr[(int64_t)bc * a.y_cols + min(o, yc - 1)];
+    }
+  }
 
-  // dF_l tile [16][g]
+  // dF_l tile [16][g]: the last layer turns F_L into the likelihood gradient in place;
+  // otherwise dF_l = dX_{l+1}[:, :g_l] (already summed above)
   if (a.last) {
     // likelihood gradient dF = -(1/B) dlogp/dF (likelihoods/gaussian.py:18-25, softmax.py:8-15)
-    const float* fpl = a.fout + (int64_t)chain * a.ws_cs;
-    const float* yr = a.yrows + (int64_t)chain * a.yrow_cs;
-    float* ysh = dfs + round4(TR * dfst);
-    const int yc = a.likelihood == DGPRF_LIK_GAUSSIAN ? g : 1;
-    for (int e = threadIdx.x; e < TR * g; e += blockDim.x) {  // F_L = sum of slices; Y alongside
-      const int r = e / g, o = e - r * g, b = row0 + r, bc = min(b, B - 1);
-      const float v = sum_slices(fpl + (int64_t)bc * g + o, (int64_t)B * g);
-      const float yv = yr[(int64_t)bc * a.y_cols + min(o, yc - 1)];
-      dfs[r * dfst + o] = b < B ? v : 0.f;
-      ysh[r * dfst + o] = yv;
-    }
     __syncthreads();
     if (threadIdx.x < TR) {
       const int r = threadIdx.x, b = row0 + r;
@@ -380,15 +517,8 @@ __global__ __launch_bounds__(256) void k_step_bwd(const LayerK a) {
         if (sl == 0) a.logp[(int64_t)chain * a.ws_cs + b] = logp;
       }
     }
-  } else {
-    // dF_l = dX_{l+1}[:, :g_l] summed over the slices of layer l+1
-    const float* dx = a.dxnext + (int64_t)chain * a.ws_cs;
-    for (int e = threadIdx.x; e < TR * g; e += blockDim.x) {
-      const int r = e / g, o = e - r * g, b = row0 + r;
-      const float v = sum_slices(dx + (int64_t)min(b, B - 1) * g + o, (int64_t)B * g);
-      dfs[r * dfst + o] = b < B ? v : 0.f;
-    }
   }
+  if (!a.fast && dxw > 0) stage_store(fb0);
   __syncthreads();
   DGPRF_STAMP(stamp_base, 2);
 
@@ -420,7 +550,12 @@ __global__ __launch_bounds__(256) void k_step_bwd(const LayerK a) {
     if (f0 >= R) break;
     if (i > 0) {
       if (KS > 0) load_om_frag<KS>(a.om, R, d, f0, lr, lq, omk);
-      if (dxw > 0) load_bwd_frag(f0);
+      if (dxw > 0) {
+        stage_load((sl * cpw + i) * 64);
+        __syncthreads();  // every wave is done with the previous block
+        stage_store((sl * cpw + i) * 64);
+        __syncthreads();
+      }
     }
     // ---- gW_l partial over this row tile: rows-in-registers orientation
     {
@@ -456,8 +591,14 @@ __global__ __launch_bounds__(256) void k_step_bwd(const LayerK a) {
 #pragma unroll
       for (int ks = 0; ks < KGM; ++ks) {
         if (ks < KG) {
-          dpc = mfma16(wdp[ks][0], dff[ks], dpc);
-          if (RBF) dps = mfma16(wdp[ks][1], dff[ks], dps);
+          const int o = 4 * ks + lq, wo = (wave * 16 + lr) * g + o;
+          const bool ok = o < g && f0 + lr < R;
+          const float w0 = ok ? wsl[wo] : 0.f;
+          dpc = mfma16(w0, dff[ks], dpc);
+          if (RBF) {
+            const float w1 = ok ? wsl[nwh + wo] : 0.f;
+            dps = mfma16(w1, dff[ks], dps);
+          }
         }
       }
       float da[4];
@@ -473,9 +614,12 @@ __global__ __launch_bounds__(256) void k_step_bwd(const LayerK a) {
       }
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt)
-        if (dt < ND)
+        if (dt < ND) {
+          // rows k >= dxw of the staged block are never written: they only feed discarded outputs
+          const f4 ox = *reinterpret_cast<const f4*>(osl + (dt * 16 + lr) * OST + wave * 16 + 4 * lq);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) dxa[dt] = mfma16(omx[dt][r], da[r], dxa[dt]);
+          for (int r = 0; r < 4; ++r) dxa[dt] = mfma16(ox[r], da[r], dxa[dt]);
+        }
     }
   }
   DGPRF_STAMP(stamp_base, 3);
@@ -664,6 +808,15 @@ LayerK make_layer_k(const dgprf_plan_t& pl, const StepDev& sd, int l, int& lds_f
   a.likelihood = pl.likelihood;
   a.layer = l;
   step_lds(a.d, a.g, a, lds_floats);
+  // element-owner prologue: X tile + dF tile <= 512 elements, W/Omega block staged by float4
+  const int dpad = round4(a.d);
+  a.ws = sd.ws;
+  a.fprev_off = l > 0 ? (int)pl.fp_off[l - 1] : 0;
+  a.dsrc_off = a.last ? (int)pl.fp_off[l] : (l + 1 < pl.n_layers ? (int)pl.dxp_off[l + 1] : 0);
+  a.fast = sd.ws != nullptr && TR * (dpad + a.g) <= 512 && a.g <= 16 && a.gp <= 16 &&
+           a.R % 4 == 0 && pl.ws_chain < (1 << 29);
+  a.xmag = div_magic(dpad);
+  a.dmag = div_magic(a.g);
   return a;
 }
 

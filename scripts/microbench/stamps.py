@@ -51,7 +51,7 @@ for k in order:
     cyc = st[:, 14] - st[:, 0]
     freq = cyc / np.maximum(real_end - real0, 1) * 100e6
     segs = []
-    marks = [i for i in range(0, 15) if (st[:, i] > 0).all()]
+    marks = [i for i in range(0, 13) if (st[:, i] > 0).all()] + [14]
     for a, b in zip(marks[:-1], marks[1:]):
         segs.append(f"{a}->{b}: {np.median(st[:, b] - st[:, a]):.0f}")
     span = (real_end.max() - real0.min()) * 10
