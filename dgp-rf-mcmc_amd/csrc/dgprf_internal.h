@@ -46,7 +46,20 @@ extern __device__ unsigned long long g_dgprf_stamps[];
       __builtin_amdgcn_sched_barrier(0);                                         \
     }                                                                            \
   } while (0)
+// per-wave placement: slots 8..11 = HW_ID | XCC_ID << 32 of waves 0..3
+#define DGPRF_STAMP_HWID(base)                                                   \
+  do {                                                                           \
+    if ((threadIdx.x & 63) == 0 && threadIdx.x < 256) {                          \
+      const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);  \
+      const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20);\
+      g_dgprf_stamps[(size_t)(base) * DGPRF_STAMP_SLOTS + 8 + (threadIdx.x >> 6)] = \
+          (unsigned long long)hw | ((unsigned long long)xcc << 32);              \
+    }                                                                            \
+  } while (0)
 #else
+#define DGPRF_STAMP_HWID(base) \
+  do {                         \
+  } while (0)
 #define DGPRF_STAMP(base, i) \
   do {                       \
     (void)(base);            \

@@ -62,20 +62,21 @@ struct LayerK {
   int32_t fast, fprev_off, dsrc_off, xmag, dmag;
 };
 
-// Arguments of the update kernel.
+// Arguments of the update kernel (hot fields first: one burst of scalar loads).
 struct UpdK {
-  float* theta;
+  float* theta;         // chain 0 (chain stride w_total)
   float* mom;
-  const float* mass;
   const float* gwp;     // gW partials base of chain 0 (chain stride ws_cs, row-tile stride w_total)
+  const float* mass;
+  const int64_t* step;
+  int32_t w_total, n_rt, n_rt_pad, n_layers;
+  int32_t lo[DGPRF_MAX_LAYERS], hi[DGPRF_MAX_LAYERS];
+  uint64_t seed;
+  int64_t ws_cs;
+  int32_t step_offset, upd_blocks;
+  UpdateDev ud;
   const float* grad_in;
   float* grad_out;
-  const int64_t* step;
-  uint64_t seed;
-  int64_t w_total, ws_cs;
-  int64_t lo[DGPRF_MAX_LAYERS], hi[DGPRF_MAX_LAYERS];
-  int32_t n_rt_pad, n_layers, step_offset, upd_blocks;
-  UpdateDev ud;
   // gather of step t+1's minibatch rows (graph mode)
   int32_t gather_next, B, d_in, yb_cols;
   BatchDev bd;
@@ -305,6 +306,7 @@ __global__ __launch_bounds__(256) void k_step_fwd(const LayerK a) {
   const int row0 = rt * TR;
   const int stamp_base = (a.layer * 2) * 4096 + (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
   DGPRF_STAMP(stamp_base, 0);
+  DGPRF_STAMP_HWID(stamp_base);
   float* xs = smem;
   float* red = smem + a.red_off;
   const float* __restrict__ W = a.W + (int64_t)chain * a.w_cs;
@@ -331,6 +333,7 @@ __global__ __launch_bounds__(256) void k_step_fwd(const LayerK a) {
   f4 acc[NOT], acs[NOT];
 #pragma unroll
   for (int ot = 0; ot < NOT; ++ot) acc[ot] = acs[ot] = f4zero();
+  DGPRF_STAMP(stamp_base, 6);
   for (int i = 0; i < cpw; ++i) {
     const int f0 = chunk_f0(i);
     if (f0 >= R) break;
@@ -357,6 +360,7 @@ __global__ __launch_bounds__(256) void k_step_fwd(const LayerK a) {
         if (RBF) acs[ot] = mfma16(wc[ot][r][1], p1[r], acs[ot]);
       }
   }
+  DGPRF_STAMP(stamp_base, 7);
   // acc[ot][r] = F[row lr][ot*16 + 4lq + r]; sum the 4 waves' feature chunks in LDS.
   constexpr int GP = NOT * 16;
   float* redw = red + wave * TR * GP;
@@ -584,6 +588,7 @@ __global__ __launch_bounds__(256) void k_step_bwd(const LayerK a) {
         }
       }
     }
+    DGPRF_STAMP(stamp_base, 6);
     if (dxw > 0) {
       // ---- dPhi = dF W^T, dA, dX = dA Omega^T : features-in-registers orientation
       const f4 at = a_tile<KS, false>(a.om, R, d, f0, omk, xf, xs, a.xst, lr, lq);
@@ -691,54 +696,89 @@ __global__ void k_gather(const GatherK a) {
              a.yb + (int64_t)chain * a.ws_cs, chain, t, b);
 }
 
-__global__ __launch_bounds__(256) void k_step_update(const UpdK a) {
+// Two N(0,1) of counter quad `quad`: words (0,1) (half 0) or (2,3) (half 1) — the same values
+// philox_normal4 returns in lanes 2*half, 2*half+1.
+__device__ __forceinline__ void philox_normal2(uint64_t seed, uint64_t sub, uint32_t purpose,
+                                               uint32_t tag, uint32_t quad, int half, float* z0,
+                                               float* z1) {
+  u32x4 c;
+  c.x = quad;
+  c.y = (uint32_t)sub;
+  c.z = (uint32_t)(sub >> 32);
+  c.w = (purpose << 24) | (tag & 0x00FFFFFFu);
+  const u32x4 r = philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  box_muller(half ? r.z : r.x, half ? r.w : r.y, z0, z1);
+}
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 ld2(const float* p) { return *reinterpret_cast<const f2*>(p); }
+__device__ __forceinline__ void st2(float* p, f2 v) { *reinterpret_cast<f2*>(p) = v; }
+
+// One wave per workgroup, two parameters per lane: the gW partial sums (16 row tiles x 8 bytes
+// per lane) are spread over >= 256 workgroups instead of concentrated on a few CUs; row tiles
+// past n_row_tiles and lanes past w_total lie outside the buffer descriptors (zero, no memory
+// traffic), so every load is issued before the first branch.  Specialised on the rarely-used
+// paths: GIN (gradient supplied), GONLY (gradient only), XI (injected noise), CYC (cyclical).
+constexpr int UPD_THREADS = 64;
+__device__ __forceinline__ f2 bload2(rsrc_t r, uint32_t byte_off) {
+  return __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(r, byte_off, 0, 0));
+}
+
+template <bool GIN, bool GONLY, bool XI, bool CYC>
+__global__ __launch_bounds__(UPD_THREADS) void k_step_update(const UpdK a) {
   const int chain = blockIdx.y;
-  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t e0 = 4 * q;
   const int stamp_base = 16 * 4096 + blockIdx.y * gridDim.x + blockIdx.x;
   DGPRF_STAMP(stamp_base, 0);
-  const UpdateDev& ud = a.ud;
-  const int64_t t = *a.step + (int64_t)a.step_offset;
   if ((int)blockIdx.x >= a.upd_blocks) {  // dedicated blocks: rows of step t+1 (off the path)
-    const int b = ((int)blockIdx.x - a.upd_blocks) * blockDim.x + threadIdx.x;
+    const int64_t t = *a.step + (int64_t)a.step_offset;
+    const int b = ((int)blockIdx.x - a.upd_blocks) * UPD_THREADS + threadIdx.x;
     if (a.gather_next && b < a.B)
       gather_row(a.bd, a.B, a.d_in, a.yb_cols, a.xb + (int64_t)chain * a.ws_cs,
                  a.yb + (int64_t)chain * a.ws_cs, chain, t + 1, b);
     return;
   }
-  if (e0 >= a.w_total) return;
-  int layer = -1;
-#pragma unroll
-  for (int l = 0; l < DGPRF_MAX_LAYERS; ++l)
-    if (l < a.n_layers && e0 >= a.lo[l] && e0 < a.hi[l]) layer = l;
-  if (layer < 0) return;
-  const int64_t base = (int64_t)chain * a.w_total + e0;
-  const float N = ud.data_size;
-  const f4 th = ld4(a.theta + base);
-  f4 gr;
-  if (a.grad_in) {
-    gr = ld4(a.grad_in + base);
+  const int e0 = 2 * ((int)blockIdx.x * UPD_THREADS + (int)threadIdx.x);
+  const uint32_t off = (uint32_t)e0 * 4u;
+  const int64_t cw = (int64_t)chain * a.w_total;
+  const rsrc_t rth = make_rsrc(a.theta + cw, a.w_total);
+  const f2 th = bload2(rth, off);
+  f2 m = {0.f, 0.f}, gr;
+  if (!GONLY) m = bload2(make_rsrc(a.mom + cw, a.w_total), off);
+  if (GIN) {
+    gr = bload2(make_rsrc(a.grad_in + cw, a.w_total), off);
   } else {
-    // sum the row-tile gW partials: groups of 16 independent loads (padding rows are zero)
-    const float* gp = a.gwp + (int64_t)chain * a.ws_cs + e0;
-    f4 s = f4zero();
+    // sum the row-tile gW partials in a fixed order: groups of 16 independent loads
+    const rsrc_t rs = make_rsrc(a.gwp + (int64_t)chain * a.ws_cs, (int64_t)a.n_rt * a.w_total);
+    f2 sacc = {0.f, 0.f};
     for (int rt0 = 0; rt0 < a.n_rt_pad; rt0 += 16) {
-      f4 v[16];
+      f2 v[16];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) v[j] = ld4(gp + (int64_t)(rt0 + j) * a.w_total);
+      for (int j = 0; j < 16; ++j) v[j] = bload2(rs, (uint32_t)(((rt0 + j) * a.w_total + e0) * 4));
 #pragma unroll
-      for (int j = 0; j < 16; ++j) s += v[j];
+      for (int j = 0; j < 16; ++j) sacc += v[j];
     }
-    // dU/dW = W/N (prior N(0,1), models/dgp.py:129-136,171) + Phi^T dF (likelihood)
-    gr = th / N + s;
+    gr = sacc;
   }
-  if (ud.grad_only) {
-    st4(a.grad_out + base, gr);
+  int layer = 0;
+#pragma unroll
+  for (int l = 1; l < DGPRF_MAX_LAYERS; ++l)
+    if (l < a.n_layers && e0 >= a.lo[l]) layer = l;
+  const bool live = e0 < a.hi[layer];  // layer padding between align4 offsets stays untouched
+  const UpdateDev& ud = a.ud;
+  const float N = ud.data_size;
+  // dU/dW = W/N (prior N(0,1), models/dgp.py:129-136,171) + Phi^T dF (likelihood)
+  if (!GIN) gr = th / N + gr;
+  if (GONLY) {
+    if (live) st2(a.grad_out + cw + e0, gr);
     return;
   }
+  const float M = a.mass[chain * a.n_layers + layer];
+  // the step counter (written by the previous step's k_advance) is read only now, after the
+  // parameter and partial loads are in flight
+  const int64_t t = *a.step + (int64_t)a.step_offset;
   float lr = ud.lr, T = ud.temperature;
   int resample = ud.resample;
-  if (ud.schedule == DGPRF_SCHED_CYCLICAL) {
+  if (CYC) {
     if (t < ud.start_step) {  // burn-in: fixed lr, zero temperature
       T = 0.f;
       resample = 0;
@@ -751,20 +791,32 @@ __global__ __launch_bounds__(256) void k_step_update(const UpdK a) {
     }
   }
   const float h = sqrtf(lr / N);
-  const float M = a.mass[chain * a.n_layers + layer];
   const float beta = ud.beta;
-  f4 m = ld4(a.mom + base);
   const uint32_t quad = (uint32_t)(e0 >> 2);
+  const int half = (e0 >> 1) & 1;
   if (resample) {  // models/dgp.py:209-210 (ignores M, Appendix A.1)
-    m = ud.xi_resample ? ld4(ud.xi_resample + base)
-                       : philox_normal4(a.seed, (uint64_t)t, DGPRF_RNG_RESAMPLE, chain, quad);
+    if (XI && ud.xi_resample) {
+      m = ld2(ud.xi_resample + cw + e0);
+    } else {
+      float z0, z1;
+      philox_normal2(a.seed, (uint64_t)t, DGPRF_RNG_RESAMPLE, chain, quad, half, &z0, &z1);
+      m = f2{z0, z1};
+    }
   }
-  f4 mn = beta * m - (h * N) * gr;
-  const f4 eps =
-      ud.xi ? ld4(ud.xi + base) : philox_normal4(a.seed, (uint64_t)t, DGPRF_RNG_NOISE, chain, quad);
+  f2 mn = beta * m - (h * N) * gr;
+  f2 eps;
+  if (XI && ud.xi) {
+    eps = ld2(ud.xi + cw + e0);
+  } else {
+    float z0, z1;
+    philox_normal2(a.seed, (uint64_t)t, DGPRF_RNG_NOISE, chain, quad, half, &z0, &z1);
+    eps = f2{z0, z1};
+  }
   mn = mn + sqrtf(2.0f * (1.0f - beta) * T * M) * eps;
-  st4(a.mom + base, mn);
-  st4(a.theta + base, th + (h * (1.0f / M)) * mn);
+  if (live) {
+    st2(a.mom + cw + e0, mn);
+    st2(a.theta + cw + e0, th + (h * (1.0f / M)) * mn);
+  }
 #ifdef DGPRF_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
@@ -892,25 +944,28 @@ hipError_t launch_step_bwd(const dgprf_plan_t& pl, const StepDev& sd, int layer,
 
 hipError_t launch_step_update(const dgprf_plan_t& pl, const StepDev& sd, const UpdateDev& ud,
                               const float* grad_in, hipStream_t s, bool gather_next) {
+  if (pl.w_total >= (int64_t)1 << 30 || (int64_t)pl.n_rt_pad * pl.w_total >= (int64_t)1 << 29)
+    return hipErrorInvalidValue;  // 32-bit buffer offsets
   UpdK a;
   a.theta = sd.theta;
   a.mom = sd.mom;
-  a.mass = sd.mass;
   a.gwp = sd.ws ? sd.ws + pl.gwp_off : nullptr;
-  a.grad_in = grad_in;
-  a.grad_out = sd.grad_out;
+  a.mass = sd.mass;
   a.step = sd.step;
-  a.seed = sd.seed;
-  a.w_total = pl.w_total;
-  a.ws_cs = pl.ws_chain;
-  for (int l = 0; l < DGPRF_MAX_LAYERS; ++l) {
-    a.lo[l] = l < pl.n_layers ? pl.w_off[l] : 0;
-    a.hi[l] = l < pl.n_layers ? pl.w_off[l] + (int64_t)pl.P[l] * pl.n_gp[l] : 0;
-  }
+  a.w_total = (int32_t)pl.w_total;
+  a.n_rt = pl.n_row_tiles;
   a.n_rt_pad = pl.n_rt_pad;
   a.n_layers = pl.n_layers;
+  for (int l = 0; l < DGPRF_MAX_LAYERS; ++l) {
+    a.lo[l] = l < pl.n_layers ? (int32_t)pl.w_off[l] : INT32_MAX;
+    a.hi[l] = l < pl.n_layers ? (int32_t)(pl.w_off[l] + (int64_t)pl.P[l] * pl.n_gp[l]) : 0;
+  }
+  a.seed = sd.seed;
+  a.ws_cs = pl.ws_chain;
   a.step_offset = sd.step_offset;
   a.ud = ud;
+  a.grad_in = grad_in;
+  a.grad_out = sd.grad_out;
   a.gather_next = gather_next && sd.bd.mode == DGPRF_BATCH_EPOCH ? 1 : 0;
   a.B = pl.batch;
   a.d_in = pl.d_in;
@@ -918,11 +973,27 @@ hipError_t launch_step_update(const dgprf_plan_t& pl, const StepDev& sd, const U
   a.bd = sd.bd;
   a.xb = sd.ws ? sd.ws + pl.xb_off : nullptr;
   a.yb = sd.ws ? sd.ws + pl.yb_off : nullptr;
-  const int64_t quads = pl.w_total / 4;
-  a.upd_blocks = (int)((quads + 255) / 256);
-  const int64_t blocks = a.upd_blocks + (a.gather_next ? (pl.batch + 255) / 256 : 0);
+  const int64_t pairs = pl.w_total / 2;
+  a.upd_blocks = (int)((pairs + UPD_THREADS - 1) / UPD_THREADS);
+  const int64_t blocks =
+      a.upd_blocks + (a.gather_next ? (pl.batch + UPD_THREADS - 1) / UPD_THREADS : 0);
   dim3 grid((unsigned)blocks, pl.n_chains);
-  hipLaunchKernelGGL(k_step_update, grid, dim3(256), 0, s, a);
+  const bool gin = grad_in != nullptr, gonly = ud.grad_only != 0;
+  const bool xi = ud.xi != nullptr || ud.xi_resample != nullptr;
+  const bool cyc = ud.schedule == DGPRF_SCHED_CYCLICAL;
+  const int sel = (gin ? 8 : 0) | (gonly ? 4 : 0) | (xi ? 2 : 0) | (cyc ? 1 : 0);
+#define DGPRF_UPD_CASE(S)                                                                     \
+  case S:                                                                                    \
+    hipLaunchKernelGGL((k_step_update<(S & 8) != 0, (S & 4) != 0, (S & 2) != 0, (S & 1) != 0>), \
+                       grid, dim3(UPD_THREADS), 0, s, a);                                    \
+    break;
+  switch (sel) {
+    DGPRF_UPD_CASE(0) DGPRF_UPD_CASE(1) DGPRF_UPD_CASE(2) DGPRF_UPD_CASE(3)
+    DGPRF_UPD_CASE(4) DGPRF_UPD_CASE(5) DGPRF_UPD_CASE(6) DGPRF_UPD_CASE(7)
+    DGPRF_UPD_CASE(8) DGPRF_UPD_CASE(9) DGPRF_UPD_CASE(10) DGPRF_UPD_CASE(11)
+    DGPRF_UPD_CASE(12) DGPRF_UPD_CASE(13) DGPRF_UPD_CASE(14) DGPRF_UPD_CASE(15)
+  }
+#undef DGPRF_UPD_CASE
   return hipGetLastError();
 }
 

@@ -51,7 +51,16 @@ for k in order:
     cyc = st[:, 14] - st[:, 0]
     freq = cyc / np.maximum(real_end - real0, 1) * 100e6
     segs = []
-    marks = [i for i in range(0, 13) if (st[:, i] > 0).all()] + [14]
+    marks = [i for i in range(0, 8) if (st[:, i] > 0).all()] + [14]
+    if (st[:, 8] > 0).all():  # placement: HW_ID (simd [5:4], cu [11:8], sh [12], se [15:13]) | XCC << 32
+        hw = st[:, 8:12]
+        simd = (hw >> 4) & 3
+        cu_key = ((hw[:, 0] >> 32) << 16) | (((hw[:, 0] >> 13) & 7) << 8) | (((hw[:, 0] >> 12) & 1) << 4) | ((hw[:, 0] >> 8) & 15)
+        uniq, cnt = np.unique(cu_key, return_counts=True)
+        simds_distinct = np.array([len(set(r)) for r in simd])
+        print(f"  placement {names[k]}: {len(uniq)} distinct CUs for {len(st)} WGs, WGs/CU max {cnt.max()}, "
+              f"distinct SIMDs per WG min {simds_distinct.min()} median {np.median(simds_distinct)}")
+    marks.sort(key=lambda i: np.median(st[:, i] - st[:, 0]))  # program order
     for a, b in zip(marks[:-1], marks[1:]):
         segs.append(f"{a}->{b}: {np.median(st[:, b] - st[:, a]):.0f}")
     span = (real_end.max() - real0.min()) * 10
