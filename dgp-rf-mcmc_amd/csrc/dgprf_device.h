@@ -29,6 +29,23 @@ __device__ __forceinline__ f4 f4zero() {
   return z;
 }
 
+// ---------------------------------------------------------------- buffer loads
+// Raw buffer loads through a wave-uniform descriptor: lanes with an offset past the descriptor's
+// size (OOB) read 0 without a memory access, so masked lanes cost no traffic and every load of a
+// burst can be unconditional.
+constexpr uint32_t DGPRF_OOB = 0x80000000u;
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+__device__ __forceinline__ rsrc_t make_rsrc(const float* p, int64_t n_floats) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)(n_floats * 4), 0x00020000);
+}
+__device__ __forceinline__ f4 bload4(rsrc_t r, uint32_t byte_off) {
+  return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
+}
+__device__ __forceinline__ float bload1(rsrc_t r, uint32_t byte_off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
+}
+
 // ---------------------------------------------------------------- Philox4x32-10
 struct u32x4 {
   uint32_t x, y, z, w;

@@ -11,6 +11,8 @@
 // Geometry: one workgroup = one 16-row tile walking ALL layers; its 4 waves split each layer's RF
 // features (16-feature chunks on v_mfma_f32_16x16x4_f32) and sum their F partials in LDS, so the
 // layer outputs never leave LDS and no cross-workgroup reduction exists.
+#include <cstdlib>
+
 #include "dgprf_internal.h"
 
 namespace {
@@ -381,6 +383,275 @@ __global__ __launch_bounds__(256) void k_prior_w(const dgprf_plan_t pl,
   if (threadIdx.x == 0) out[chain] = total;
 }
 
+
+// ============================================================================ tile kernel
+// k_forward_tiles: the same computation as k_forward_rows for models whose layers all have
+// d <= 32, g <= 64 and R % 4 == 0 (every configuration of BASELINE.json).
+//   * a workgroup covers 64 rows: each wave owns a 16-row tile through ALL layers, so F accumulates
+//     in the wave's registers over the whole feature loop — no cross-wave reduction;
+//   * the 4 waves walk the same 64-feature blocks: each block's Omega rows (d x 64) and W rows
+//     (2 x 64 x g) are fetched once per workgroup with buffer_load_dwordx4 into a double-buffered
+//     LDS ring (the next block's loads are in flight while the current block computes), one barrier
+//     per block;
+//   * the layer output F (16 x g per wave) stays in the wave's LDS tile and is the next layer's
+//     input; dataset columns ([F | X], utils.py:42) come from the wave's X rows, loaded once.
+constexpr int TW_ROWS = NW * TR;  // rows per workgroup
+#ifndef DGPRF_TILE_WAVES
+#define DGPRF_TILE_WAVES 4  // waves per SIMD the register budget must allow (latency hiding)
+#endif
+constexpr int TW_OST = 80;        // LDS row stride of a staged Omega block (conflict-free reads)
+
+struct TileLds {
+  int obuf, wbuf, o_off, w_off, xin_off, xin_st, f_off, ftst, total;
+};
+
+__host__ __device__ inline TileLds tile_lds(const dgprf_plan_t& pl, int njw, int njo) {
+  int gmax = 1;
+  for (int l = 0; l < pl.n_layers; ++l) gmax = pl.n_gp[l] > gmax ? pl.n_gp[l] : gmax;
+  TileLds T;
+  T.obuf = 16 * njo * TW_OST;                                  // njo float4 per thread: 16 rows each
+  T.wbuf = (2 * 64 * gmax > 1024 * njw) ? 2 * 64 * gmax : 1024 * njw;
+  T.o_off = 0;
+  T.w_off = 2 * T.obuf;
+  T.xin_st = round4(pl.d_in);
+  T.xin_off = T.w_off + 2 * T.wbuf;
+  T.ftst = gmax + 1;
+  T.f_off = T.xin_off + NW * TR * T.xin_st;
+  T.total = T.f_off + NW * round4(TR * T.ftst);
+  return T;
+}
+
+// One layer for the calling wave's 16 rows.  JW / JO: float4 W / Omega loads per thread per block.
+template <int NOT, bool RBF, bool G1, int JW, int JO>
+__device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
+                                           const float* __restrict__ W,
+                                           const float* __restrict__ om, float cl,
+                                           const TileLds& T, float* smem, float* xin, float* ftw,
+                                           int wave, int lr, int lq, int64_t wrow0, int64_t n,
+                                           float* fout) {
+  const int d = pl.d[layer], R = pl.n_rf[layer], g = pl.n_gp[layer];
+  const int gp = layer > 0 ? pl.n_gp[layer - 1] : 0;
+  const int tid = threadIdx.x;
+  // x fragments of the A = Omega^T x contraction: xf[ks] = X_l[row lr][4ks + lq]
+  float xf[8];
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) {
+    const int col = 4 * ks + lq;
+    float v = 0.f;
+    if (4 * ks < d) {
+      const float a = ftw[lr * T.ftst + min(col, T.ftst - 1)];
+      const float b = xin[lr * T.xin_st + min(max(col - gp, 0), T.xin_st - 1)];
+      v = col < gp ? a : (col < d ? b : 0.f);
+    }
+    xf[ks] = v;
+  }
+  const rsrc_t rw = make_rsrc(W, (int64_t)(RBF ? 2 : 1) * R * g);
+  const rsrc_t ro = make_rsrc(om, (int64_t)d * R);
+  const int nwq = (RBF ? 32 : 16) * g;  // float4 of one W block
+  f4 sw[JW], so[JO];
+  auto stage_load = [&](int fb) {
+#pragma unroll
+    for (int j = 0; j < JW; ++j) {
+      const int i = tid + 256 * j, h = i >= 16 * g, q = i - h * 16 * g;
+      sw[j] = bload4(rw, i < nwq ? (uint32_t)((((h * R) + fb) * g + 4 * q) * 4) : DGPRF_OOB);
+    }
+#pragma unroll
+    for (int j = 0; j < JO; ++j) {
+      const int i = tid + 256 * j, k = i >> 4, c4 = i & 15;
+      so[j] = bload4(ro, k < d && fb + 4 * c4 < R ? (uint32_t)((k * R + fb + 4 * c4) * 4) : DGPRF_OOB);
+    }
+  };
+  auto stage_store = [&](int buf) {
+    float* wsb = smem + T.w_off + buf * T.wbuf;
+    float* osb = smem + T.o_off + buf * T.obuf;
+#pragma unroll
+    for (int j = 0; j < JW; ++j) *reinterpret_cast<f4*>(wsb + 4 * (tid + 256 * j)) = sw[j];
+#pragma unroll
+    for (int j = 0; j < JO; ++j) {
+      const int i = tid + 256 * j;
+      *reinterpret_cast<f4*>(osb + (i >> 4) * TW_OST + 4 * (i & 15)) = so[j];
+    }
+  };
+
+  f4 acc[NOT], acs[NOT];
+#pragma unroll
+  for (int ot = 0; ot < NOT; ++ot) acc[ot] = acs[ot] = f4zero();
+  float dot = 0.f;
+  const int nb = (R + 63) >> 6;
+  stage_load(0);
+  stage_store(0);
+  __syncthreads();
+  for (int blk = 0; blk < nb; ++blk) {
+    const int fb = blk * 64, buf = blk & 1;
+    if (blk + 1 < nb) stage_load(fb + 64);
+    const float* wsb = smem + T.w_off + buf * T.wbuf;
+    const float* osb = smem + T.o_off + buf * T.obuf;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      // A[row lr][feature fb + 16c + 4lq + r]
+      f4 at = f4zero();
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks)
+        if (4 * ks < d) at = mfma16(osb[(4 * ks + lq) * TW_OST + 16 * c + lr], xf[ks], at);
+      float p0[4], p1[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (RBF) {
+          float sv, cv;
+          rf_sincos(at[r], &sv, &cv);
+          p0[r] = cl * cv;
+          p1[r] = cl * sv;
+        } else {
+          p0[r] = cl * fmaxf(at[r], 0.f);
+          p1[r] = 0.f;
+        }
+      }
+      const int fl = 16 * c + 4 * lq;  // first feature of this lane within the block
+      if (G1) {
+        const f4 w0 = *reinterpret_cast<const f4*>(wsb + fl);
+        const f4 w1 = RBF ? *reinterpret_cast<const f4*>(wsb + 64 + fl) : f4zero();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float m = fb + fl + r < R ? 1.f : 0.f;
+          dot = fmaf(p0[r], w0[r] * m, dot);
+          if (RBF) dot = fmaf(p1[r], w1[r] * m, dot);
+        }
+      } else {
+#pragma unroll
+        for (int ot = 0; ot < NOT; ++ot) {
+          const int o = ot * 16 + lr;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const bool ok = o < g && fb + fl + r < R;
+            const int wi = (fl + r) * g + min(o, g - 1);
+            const float w0 = ok ? wsb[wi] : 0.f;
+            acc[ot] = mfma16(w0, p0[r], acc[ot]);
+            if (RBF) {
+              const float w1 = ok ? wsb[64 * g + wi] : 0.f;
+              acs[ot] = mfma16(w1, p1[r], acs[ot]);
+            }
+          }
+        }
+      }
+    }
+    if (blk + 1 < nb) stage_store(buf ^ 1);
+    __syncthreads();
+  }
+  // F tile of this wave -> ftw (the next layer's input) and the optional per-layer output
+  if (G1) {
+    dot += __shfl_xor(dot, 16);
+    dot += __shfl_xor(dot, 32);
+    if (lq == 0) {
+      ftw[lr * T.ftst] = dot;
+      if (fout && wrow0 + lr < n) fout[wrow0 + lr] = dot;
+    }
+  } else {
+    // acc[ot][r] = F[row lr][ot*16 + 4lq + r]
+#pragma unroll
+    for (int ot = 0; ot < NOT; ++ot)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int o = ot * 16 + 4 * lq + r;
+        if (o < g) {
+          const float v = acc[ot][r] + acs[ot][r];
+          ftw[lr * T.ftst + o] = v;
+          if (fout && wrow0 + lr < n) fout[(wrow0 + lr) * g + o] = v;
+        }
+      }
+  }
+  __syncthreads();  // ftw complete before the next layer reads its x fragments
+}
+
+template <int NOTMAX, int JW, int JO>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DGPRF_TILE_WAVES)))
+void k_forward_tiles(
+    const dgprf_plan_t pl, const float* __restrict__ theta, const float* __restrict__ omega,
+    const float* __restrict__ der, const float* __restrict__ X, const float* __restrict__ Y,
+    const int y_cols, const int64_t n, const FOut fo, float* __restrict__ logp_out,
+    float* __restrict__ se_out, float* __restrict__ lse_m, float* __restrict__ lse_s,
+    float* __restrict__ se_sum) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const TileLds T = tile_lds(pl, JW, JO);
+  const int chain = blockIdx.y;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, lr = lane & 15, lq = lane >> 4;
+  const int64_t wrow0 = (int64_t)blockIdx.x * TW_ROWS + wave * TR;
+  float* xin = smem + T.xin_off + wave * TR * T.xin_st;
+  float* ftw = smem + T.f_off + wave * round4(TR * T.ftst);
+  const float* Wc = theta + (int64_t)chain * pl.w_total;
+  const int L = pl.n_layers;
+  // this wave's X rows (zero past n)
+  for (int e = lane; e < TR * T.xin_st; e += 64) {
+    const int r = e / T.xin_st, k = e - r * T.xin_st;
+    const int64_t b = wrow0 + r;
+    xin[e] = (b < n && k < pl.d_in) ? X[b * pl.d_in + k] : 0.f;
+  }
+  for (int e = lane; e < TR * T.ftst; e += 64) ftw[e] = 0.f;
+  __syncthreads();
+  for (int layer = 0; layer < L; ++layer) {
+    const float* __restrict__ om = omega + pl.omega_off[layer];
+    const float* __restrict__ W = Wc + pl.w_off[layer];
+    const float cl = der[layer];
+    const int g = pl.n_gp[layer], NOT = (g + 15) >> 4;
+    const bool rbf = pl.kind[layer] == DGPRF_RBF;
+    float* fout = fo.p[layer] ? fo.p[layer] + (int64_t)chain * n * g : nullptr;
+#define DGPRF_TL(NT, RB, G1_)                                                                  \
+  tile_layer<NT, RB, G1_, JW, JO>(pl, layer, W, om, cl, T, smem, xin, ftw, wave, lr, lq, wrow0, n, \
+                              fout)
+    if (g == 1) {
+      if (rbf) DGPRF_TL(1, true, true);
+      else DGPRF_TL(1, false, true);
+    } else if (NOT == 1) {
+      if (rbf) DGPRF_TL(1, true, false);
+      else DGPRF_TL(1, false, false);
+    } else if (NOTMAX >= 2 && NOT == 2) {
+      if (rbf) DGPRF_TL((NOTMAX >= 2 ? 2 : 1), true, false);
+      else DGPRF_TL((NOTMAX >= 2 ? 2 : 1), false, false);
+    } else if (NOTMAX >= 4) {
+      if (rbf) DGPRF_TL((NOTMAX >= 4 ? 4 : 1), true, false);
+      else DGPRF_TL((NOTMAX >= 4 ? 4 : 1), false, false);
+    }
+#undef DGPRF_TL
+  }
+  // likelihood per row: lanes 0..15 of each wave, row lr of the wave's tile
+  const bool want_lik = logp_out || se_out || lse_m;
+  if (want_lik && lq == 0) {
+    const int64_t b = wrow0 + lr;
+    if (b < n) {
+      const int g = pl.n_gp[L - 1];
+      const float* f = ftw + lr * T.ftst;
+      const float* y = Y + b * y_cols;
+      float lp = 0.f, se = 0.f;
+      if (pl.likelihood == DGPRF_LIK_GAUSSIAN) {
+        const float var = der[DGPRF_MAX_LAYERS];
+        const float logvar = logf(var);
+        for (int o = 0; o < g; ++o) {
+          const float diff = y[o] - f[o];
+          lp += -0.5f * (LOG_2PI + logvar + diff * diff / var);
+          se += diff * diff;
+        }
+        se = se / (float)g;  // reduce_mean over outputs (regression_model.py:46)
+      } else {
+        float mx = -INFINITY;
+        for (int o = 0; o < g; ++o) mx = fmaxf(mx, f[o]);
+        float s = 0.f;
+        for (int o = 0; o < g; ++o) s += expf(f[o] - mx);
+        const int label = min(max((int)y[0], 0), g - 1);
+        lp = f[label] - (mx + logf(s));
+      }
+      const int64_t idx = (int64_t)chain * n + b;
+      if (logp_out) logp_out[idx] = lp;
+      if (se_out) se_out[idx] = se;
+      if (lse_m) {
+        const float m0 = lse_m[idx], s0 = lse_s[idx];
+        const float m1 = fmaxf(m0, lp);
+        lse_s[idx] = s0 * expf(m0 - m1) + expf(lp - m1);
+        lse_m[idx] = m1;
+        if (se_sum) se_sum[idx] += se;
+      }
+    }
+  }
+}
+
 }  // namespace
 
 namespace dgprf {
@@ -398,6 +669,44 @@ hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const
   for (int l = 0; l < pl.n_layers; ++l) {
     smalld = smalld && pl.d[l] <= 32;
     notmax = max(notmax, (pl.n_gp[l] + 15) >> 4);
+  }
+  // tile kernel: d <= 32, g <= 64, R % 4 == 0 in every layer, d_in <= 32
+  bool tiles = pl.d_in <= 32;
+  for (int l = 0; l < pl.n_layers; ++l)
+    tiles = tiles && pl.d[l] <= 32 && pl.n_gp[l] <= 64 && pl.n_rf[l] % 4 == 0 &&
+            (int64_t)2 * pl.n_rf[l] * pl.n_gp[l] < ((int64_t)1 << 29);
+  if (tiles && !getenv("DGPRF_FORWARD_ROWS")) {
+    int gmax = 1, dmax = 1;
+    for (int l = 0; l < pl.n_layers; ++l) {
+      gmax = max(gmax, pl.n_gp[l]);
+      dmax = max(dmax, pl.d[l]);
+    }
+    const int njw = gmax <= 8 ? 1 : (gmax <= 16 ? 2 : (gmax <= 32 ? 4 : 8));  // >= 32 g / 256
+    // >= 16 d / 256; the wide-g instances are compiled with JO = 2 only (host and kernel must size
+    // the LDS ring identically)
+    const int njo = (dmax <= 16 && njw <= 2) ? 1 : 2;
+    const TileLds T = tile_lds(pl, njw, njo);
+    dim3 tgrid((unsigned)((n + TW_ROWS - 1) / TW_ROWS), pl.n_chains);
+    const size_t tl = (size_t)T.total * sizeof(float);
+#define DGPRF_TILE_LAUNCH(NM, J, JO)                                                               \
+  do {                                                                                             \
+    set_lds_limit((const void*)k_forward_tiles<NM, J, JO>, tl);                                    \
+    hipLaunchKernelGGL((k_forward_tiles<NM, J, JO>), tgrid, dim3(256), tl, s, pl, theta, omega,    \
+                       der, X, Y, y_cols, n, fo, logp, se, lse_m, lse_s, se_sum);                  \
+  } while (0)
+    if (njw == 1) {
+      if (njo == 1) DGPRF_TILE_LAUNCH(1, 1, 1);
+      else DGPRF_TILE_LAUNCH(1, 1, 2);
+    } else if (njw == 2) {
+      if (njo == 1) DGPRF_TILE_LAUNCH(1, 2, 1);
+      else DGPRF_TILE_LAUNCH(1, 2, 2);
+    } else if (njw == 4) {
+      DGPRF_TILE_LAUNCH(2, 4, 2);
+    } else {
+      DGPRF_TILE_LAUNCH(4, 8, 2);
+    }
+#undef DGPRF_TILE_LAUNCH
+    return hipGetLastError();
   }
   dim3 grid((unsigned)((n + TR - 1) / TR), pl.n_chains);
   const size_t lds = (size_t)LD.total * sizeof(float);

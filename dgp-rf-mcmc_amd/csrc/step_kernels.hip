@@ -60,7 +60,20 @@ struct LayerK {
   // element-owner prologue (fast == 1): workspace offsets of the partial buffers, magic divisors
   const float* ws;      // chain 0 workspace (chain stride ws_cs)
   int32_t fast, fprev_off, dsrc_off, xmag, dmag;
+  int32_t n_rt, ns, rt_per_xcd;  // XCD-aware block -> (row tile, slice) map
 };
+
+// Block -> (row tile, slice): blocks are dealt round-robin over the 8 XCDs, so block b's XCD group
+// is b % 8; every workgroup of row tile rt gets group rt % 8, so the slice partials it exchanges
+// with the neighbouring layers' kernels stay within one L2.  Speed only: correctness never depends
+// on placement.  Blocks past the last row tile exit at once.
+__device__ __forceinline__ bool tile_of_block(const LayerK& a, int& rt, int& sl) {
+  const int b = blockIdx.x, grp = b & 7, idx = b >> 3;
+  const int j = idx / a.ns;
+  sl = idx - j * a.ns;
+  rt = grp + 8 * j;
+  return rt < a.n_rt;
+}
 
 // Arguments of the update kernel (hot fields first: one burst of scalar loads).
 struct UpdK {
@@ -113,22 +126,6 @@ __host__ __device__ inline void step_lds(int d, int g, LayerK& a, int& total) {
 // floor(i / n) = (i * magic(n)) >> 20 for 0 <= i < 4096, 1 <= n <= 256
 __host__ __device__ inline int div_magic(int n) { return (int)((1048576 + n - 1) / n); }
 
-// ---- single-burst prologue: every operand tile of a workgroup is fetched with one
-// buffer_load_dwordx4 per 16 bytes (no redundant lanes; lanes past a tile get an out-of-range
-// offset, which returns 0 without a memory access), all loads issued before the first wait.
-constexpr uint32_t OOB = 0x80000000u;
-typedef __amdgpu_buffer_rsrc_t rsrc_t;
-
-__device__ __forceinline__ rsrc_t make_rsrc(const float* p, int64_t n_floats) {
-  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)(n_floats * 4), 0x00020000);
-}
-__device__ __forceinline__ f4 bload4(rsrc_t r, uint32_t byte_off) {
-  return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
-}
-__device__ __forceinline__ float bload1(rsrc_t r, uint32_t byte_off) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
-}
-
 // X_l[16][d] of batch rows row0..: F_{l-1} partial sums (+ [F | X] dataset columns for input_cat,
 // utils.py:42) or the gathered minibatch rows for layer 0.
 __device__ __forceinline__ void load_x_tile(const LayerK& a, int chain, int row0, float* xs) {
@@ -179,12 +176,12 @@ __device__ __forceinline__ void elem_issue(const LayerK& a, int chain, int row0,
   const int str = a.B * w;
 #pragma unroll
   for (int sl = 0; sl < NSM; ++sl)
-    e.v[sl] = bload1(rws, fromp ? (uint32_t)((base + sl * str) * 4) : OOB);
+    e.v[sl] = bload1(rws, fromp ? (uint32_t)((base + sl * str) * 4) : DGPRF_OOB);
   const bool xdat = inb && isx && c >= a.gp && c < a.d;
-  e.xd = bload1(rx, xdat ? (uint32_t)((b * ndat + (c - a.gp)) * 4) : OOB);
+  e.xd = bload1(rx, xdat ? (uint32_t)((b * ndat + (c - a.gp)) * 4) : DGPRF_OOB);
   const int yc = a.likelihood == DGPRF_LIK_GAUSSIAN ? a.g : 1;
   const bool ydat = inb && isd && a.last;
-  e.y = bload1(ry, ydat ? (uint32_t)((b * a.y_cols + min(c, yc - 1)) * 4) : OOB);
+  e.y = bload1(ry, ydat ? (uint32_t)((b * a.y_cols + min(c, yc - 1)) * 4) : DGPRF_OOB);
   e.isx = isx;
   e.dst = isx ? r * a.xst + c : (isd ? r * dfst + c : -1);
 }
@@ -275,38 +272,40 @@ __device__ __forceinline__ float om_safe(const float* __restrict__ om, int R, in
   return om[(int64_t)min(k, rows - 1) * R + min(f, R - 1)];
 }
 
-// W fragments for F^T += W^T Phi^T: wf[ot][r][0|1] = W[f0+4lq+r (| R+...)][ot*16+lr]
-template <int NOT, bool RBF>
+// W fragments for F^T += W^T Phi^T: wf[ot][r][0|1] = W[f0+4lq+r (| R+...)][ot*16+lr] (G1: column
+// 0 in every lane), clamped raw loads; the caller masks at the point of use (w_ok), so a prefetch
+// never waits on its own loads.
+template <int NOT, bool RBF, bool G1>
 __device__ __forceinline__ void load_w_frag(const float* __restrict__ W, int R, int g, int f0,
                                             int lr, int lq, float (&wf)[NOT][4][2]) {
 #pragma unroll
   for (int ot = 0; ot < NOT; ++ot) {
-    const int o = ot * 16 + lr, oc = min(o, g - 1);
+    const int oc = G1 ? 0 : min(ot * 16 + lr, g - 1);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int fr = f0 + 4 * lq + r, fc = min(fr, R - 1);
-      const bool ok = o < g && fr < R;
-      wf[ot][r][0] = keep(W[(int64_t)fc * g + oc], ok);
-      if (RBF) {
-        wf[ot][r][1] = keep(W[(int64_t)(R + fc) * g + oc], ok);
-      } else {
-        wf[ot][r][1] = 0.f;
-      }
+      const int fc = min(f0 + 4 * lq + r, R - 1);
+      wf[ot][r][0] = W[(int64_t)fc * g + oc];
+      wf[ot][r][1] = RBF ? W[(int64_t)(R + fc) * g + oc] : 0.f;
     }
   }
 }
+template <bool G1>
+__device__ __forceinline__ bool w_ok(int ot, int r, int R, int g, int f0, int lr, int lq) {
+  return (G1 || ot * 16 + lr < g) && f0 + 4 * lq + r < R;
+}
 
 // ------------------------------------------------------------------------- forward
-template <int KS, int NOT, bool RBF>
+template <int KS, int NOT, bool RBF, bool G1>
 __global__ __launch_bounds__(256) void k_step_fwd(const LayerK a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int chain = blockIdx.z, rt = blockIdx.x, sl = blockIdx.y;
+  int rt, sl;
+  if (!tile_of_block(a, rt, sl)) return;
+  const int chain = blockIdx.z;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, lr = lane & 15, lq = lane >> 4;
   const int R = a.R, g = a.g, d = a.d, B = a.B, cpw = a.cpw;
   const int row0 = rt * TR;
-  const int stamp_base = (a.layer * 2) * 4096 + (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+  const int stamp_base = (a.layer * 2) * 4096 + blockIdx.z * gridDim.x + blockIdx.x;
   DGPRF_STAMP(stamp_base, 0);
-  DGPRF_STAMP_HWID(stamp_base);
   float* xs = smem;
   float* red = smem + a.red_off;
   const float* __restrict__ W = a.W + (int64_t)chain * a.w_cs;
@@ -315,7 +314,7 @@ __global__ __launch_bounds__(256) void k_step_fwd(const LayerK a) {
   // first chunk's fragments: independent of the X tile, issued first
   float omk[8], wf[NOT][4][2];
   if (KS > 0) load_om_frag<KS>(a.om, R, d, chunk_f0(0), lr, lq, omk);
-  load_w_frag<NOT, RBF>(W, R, g, chunk_f0(0), lr, lq, wf);
+  load_w_frag<NOT, RBF, G1>(W, R, g, chunk_f0(0), lr, lq, wf);
   const float cl = *a.cptr;
   DGPRF_STAMP(stamp_base, 1);
   if (a.fast) {
@@ -333,6 +332,7 @@ __global__ __launch_bounds__(256) void k_step_fwd(const LayerK a) {
   f4 acc[NOT], acs[NOT];
 #pragma unroll
   for (int ot = 0; ot < NOT; ++ot) acc[ot] = acs[ot] = f4zero();
+  float acc1 = 0.f;  // G1: per-lane partial of F[row lr]
   DGPRF_STAMP(stamp_base, 6);
   for (int i = 0; i < cpw; ++i) {
     const int f0 = chunk_f0(i);
@@ -345,29 +345,45 @@ __global__ __launch_bounds__(256) void k_step_fwd(const LayerK a) {
     for (int ot = 0; ot < NOT; ++ot)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        wc[ot][r][0] = wf[ot][r][0];
-        wc[ot][r][1] = wf[ot][r][1];
+        const bool ok = w_ok<G1>(ot, r, R, g, f0, lr, lq);
+        wc[ot][r][0] = keep(wf[ot][r][0], ok);
+        wc[ot][r][1] = keep(wf[ot][r][1], ok);
       }
     if (i + 1 < cpw) {  // prefetch the next chunk (clamped loads are always in range)
       if (KS > 0) load_om_frag<KS>(a.om, R, d, chunk_f0(i + 1), lr, lq, omk);
-      load_w_frag<NOT, RBF>(W, R, g, chunk_f0(i + 1), lr, lq, wf);
+      load_w_frag<NOT, RBF, G1>(W, R, g, chunk_f0(i + 1), lr, lq, wf);
     }
-#pragma unroll
-    for (int ot = 0; ot < NOT; ++ot)
+    if (G1) {
+      // g == 1: F[row lr] += sum_f Phi[lr][f] W[f], 4 features per lane (VALU)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        acc[ot] = mfma16(wc[ot][r][0], p0[r], acc[ot]);
-        if (RBF) acs[ot] = mfma16(wc[ot][r][1], p1[r], acs[ot]);
+        acc1 = fmaf(p0[r], wc[0][r][0], acc1);
+        if (RBF) acc1 = fmaf(p1[r], wc[0][r][1], acc1);
       }
+    } else {
+#pragma unroll
+      for (int ot = 0; ot < NOT; ++ot)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          acc[ot] = mfma16(wc[ot][r][0], p0[r], acc[ot]);
+          if (RBF) acs[ot] = mfma16(wc[ot][r][1], p1[r], acs[ot]);
+        }
+    }
   }
   DGPRF_STAMP(stamp_base, 7);
   // acc[ot][r] = F[row lr][ot*16 + 4lq + r]; sum the 4 waves' feature chunks in LDS.
   constexpr int GP = NOT * 16;
   float* redw = red + wave * TR * GP;
+  if (G1) {
+    acc1 += __shfl_xor(acc1, 16);
+    acc1 += __shfl_xor(acc1, 32);
+    if (lq == 0) redw[lr * GP] = acc1;
+  } else {
 #pragma unroll
-  for (int ot = 0; ot < NOT; ++ot)
+    for (int ot = 0; ot < NOT; ++ot)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) redw[lr * GP + ot * 16 + 4 * lq + r] = acc[ot][r] + acs[ot][r];
+      for (int r = 0; r < 4; ++r) redw[lr * GP + ot * 16 + 4 * lq + r] = acc[ot][r] + acs[ot][r];
+  }
   DGPRF_STAMP(stamp_base, 3);
   __syncthreads();
   float* fp = a.fout + (int64_t)chain * a.ws_cs + (int64_t)sl * B * g;
@@ -387,14 +403,16 @@ __global__ __launch_bounds__(256) void k_step_fwd(const LayerK a) {
 }
 
 // ------------------------------------------------------------------------- backward
-template <int KS, int NOT, bool RBF>
+template <int KS, int NOT, bool RBF, bool G1>
 __global__ __launch_bounds__(256) void k_step_bwd(const LayerK a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int chain = blockIdx.z, rt = blockIdx.x, sl = blockIdx.y;
+  int rt, sl;
+  if (!tile_of_block(a, rt, sl)) return;
+  const int chain = blockIdx.z;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, lr = lane & 15, lq = lane >> 4;
   const int R = a.R, g = a.g, d = a.d, B = a.B, cpw = a.cpw, dxw = a.dxw;
   const int row0 = rt * TR;
-  const int stamp_base = (a.layer * 2 + 1) * 4096 + (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+  const int stamp_base = (a.layer * 2 + 1) * 4096 + blockIdx.z * gridDim.x + blockIdx.x;
   DGPRF_STAMP(stamp_base, 0);
   float* xs = smem;
   float* dfs = smem + a.aux_off;
@@ -460,11 +478,11 @@ __global__ __launch_bounds__(256) void k_step_bwd(const LayerK a) {
       for (int j = 0; j < 2; ++j) {
         const int i = (int)threadIdx.x + 256 * j, h = i >= 16 * g, q = i - h * 16 * g;
         const uint32_t off = (uint32_t)((((h * R) + fb0) * g + 4 * q) * 4);
-        sw[j] = bload4(rw, i < (RBF ? 32 : 16) * g ? off : OOB);
+        sw[j] = bload4(rw, i < (RBF ? 32 : 16) * g ? off : DGPRF_OOB);
       }
       const rsrc_t ro = make_rsrc(a.om, (int64_t)dxw * R);
       const int k = threadIdx.x >> 4, c4 = threadIdx.x & 15;
-      so = bload4(ro, k < dxw && fb0 + 4 * c4 < R ? (uint32_t)((k * R + fb0 + 4 * c4) * 4) : OOB);
+      so = bload4(ro, k < dxw && fb0 + 4 * c4 < R ? (uint32_t)((k * R + fb0 + 4 * c4) * 4) : DGPRF_OOB);
     }
     DGPRF_STAMP(stamp_base, 1);
     elem_prologue(a, chain, row0, TR * g, xs, dfs, dfst, ysh, red);
@@ -546,6 +564,11 @@ __global__ __launch_bounds__(256) void k_step_bwd(const LayerK a) {
       dfg[ot][r] = (o < g) ? dfs[(4 * lq + r) * dfst + o] : 0.f;
     }
   const int KG = (g + 3) >> 2;
+  // g == 1 operands: dF[row lr] and dF[rows 4lq..4lq+3] in every lane
+  const float dg1 = G1 ? dfs[lr * dfst] : 0.f;
+  float dg4[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) dg4[r] = G1 ? dfs[(4 * lq + r) * dfst] : 0.f;
 
   float* gwp = a.gwp + (int64_t)chain * a.ws_cs + (int64_t)rt * a.w_cs;
   f4 dxa[4] = {f4zero(), f4zero(), f4zero(), f4zero()};
@@ -561,11 +584,87 @@ __global__ __launch_bounds__(256) void k_step_bwd(const LayerK a) {
         __syncthreads();
       }
     }
-    // ---- gW_l partial over this row tile: rows-in-registers orientation
-    {
-      const f4 at = a_tile<KS, true>(a.om, R, d, f0, omk, xf, xs, a.xst, lr, lq);
-      float q0[4], q1[4];
-      features<RBF>(at, cl, q0, q1);
+    // ---- phase 1: LDS operands, both A-tile orientations and dPhi (independent chains)
+    //   at_t: rows in registers  (gW = Phi^T dF,   K = rows)
+    //   at_n: features in registers (dA -> dX = dA Omega^T, K = features)
+    //   dPhi = dF W^T in the features-in-registers orientation (K = g)
+    float wd0[KGM], wd1[KGM];
+    f4 oxv[4];
+    if (dxw > 0) {
+      const bool frow = f0 + lr < R;
+#pragma unroll
+      for (int ks = 0; ks < KGM; ++ks) {
+        const int o = 4 * ks + lq, wo = (wave * 16 + lr) * g + o;
+        const bool ok = o < g && frow;
+        wd0[ks] = G1 ? 0.f : (ok ? wsl[wo] : 0.f);
+        wd1[ks] = (G1 || !RBF) ? 0.f : (ok ? wsl[nwh + wo] : 0.f);
+      }
+      // rows k >= dxw of the staged block are never written: they only feed discarded outputs
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+        oxv[dt] = *reinterpret_cast<const f4*>(osl + (dt * 16 + lr) * OST + wave * 16 + 4 * lq);
+    }
+    const f4 at_t = a_tile<KS, true>(a.om, R, d, f0, omk, xf, xs, a.xst, lr, lq);
+    f4 at_n = f4zero(), dpc = f4zero(), dps = f4zero();
+    if (dxw > 0) {
+      at_n = a_tile<KS, false>(a.om, R, d, f0, omk, xf, xs, a.xst, lr, lq);
+      if (G1) {
+        // g == 1: dPhi[b][f] = dF[b] W[f] (outer product, VALU)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int fl = wave * 16 + 4 * lq + r;
+          const bool ok = f0 + 4 * lq + r < R;
+          dpc[r] = ok ? dg1 * wsl[fl] : 0.f;
+          dps[r] = (ok && RBF) ? dg1 * wsl[64 + fl] : 0.f;
+        }
+      } else {
+#pragma unroll
+        for (int ks = 0; ks < KGM; ++ks) {
+          if (ks < KG) {
+            dpc = mfma16(wd0[ks], dff[ks], dpc);
+            if (RBF) dps = mfma16(wd1[ks], dff[ks], dps);
+          }
+        }
+      }
+    }
+    // ---- phase 2: transcendentals of both tiles, batched
+    float q0[4], q1[4];
+    features<RBF>(at_t, cl, q0, q1);
+    float da[4];
+    if (dxw > 0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (RBF) {
+          float sv, cv;
+          rf_sincos(at_n[r], &sv, &cv);
+          da[r] = -(cl * sv) * dpc[r] + (cl * cv) * dps[r];
+        } else {
+          da[r] = at_n[r] > 0.f ? cl * dpc[r] : 0.f;
+        }
+      }
+    }
+    DGPRF_STAMP(stamp_base, 8);
+    // ---- phase 3: gW_l partial of this row tile, then dX
+    if (G1) {
+      // g == 1: gW[f] = sum_b Phi[b][f] dF[b]: 4 rows per lane, then across the 4 row groups
+      float gc = 0.f, gs = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        gc = fmaf(q0[r], dg4[r], gc);
+        if (RBF) gs = fmaf(q1[r], dg4[r], gs);
+      }
+      gc += __shfl_xor(gc, 16);
+      gc += __shfl_xor(gc, 32);
+      if (RBF) {
+        gs += __shfl_xor(gs, 16);
+        gs += __shfl_xor(gs, 32);
+      }
+      const int f = f0 + lr;
+      if (lq == 0 && f < R) {
+        gwp[f] = gc;
+        if (RBF) gwp[R + f] = gs;
+      }
+    } else {
 #pragma unroll
       for (int ot = 0; ot < NOT; ++ot) {
         f4 gc = f4zero(), gs = f4zero();
@@ -574,6 +673,7 @@ __global__ __launch_bounds__(256) void k_step_bwd(const LayerK a) {
           gc = mfma16(q0[r], dfg[ot][r], gc);
           if (RBF) gs = mfma16(q1[r], dfg[ot][r], gs);
         }
+        DGPRF_STAMP(stamp_base, 9);
         // gc[r] = gW[f0 + 4lq + r][ot*16 + lr]
         const int o = ot * 16 + lr;
         if (o < g) {
@@ -590,40 +690,11 @@ __global__ __launch_bounds__(256) void k_step_bwd(const LayerK a) {
     }
     DGPRF_STAMP(stamp_base, 6);
     if (dxw > 0) {
-      // ---- dPhi = dF W^T, dA, dX = dA Omega^T : features-in-registers orientation
-      const f4 at = a_tile<KS, false>(a.om, R, d, f0, omk, xf, xs, a.xst, lr, lq);
-      f4 dpc = f4zero(), dps = f4zero();
-#pragma unroll
-      for (int ks = 0; ks < KGM; ++ks) {
-        if (ks < KG) {
-          const int o = 4 * ks + lq, wo = (wave * 16 + lr) * g + o;
-          const bool ok = o < g && f0 + lr < R;
-          const float w0 = ok ? wsl[wo] : 0.f;
-          dpc = mfma16(w0, dff[ks], dpc);
-          if (RBF) {
-            const float w1 = ok ? wsl[nwh + wo] : 0.f;
-            dps = mfma16(w1, dff[ks], dps);
-          }
-        }
-      }
-      float da[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (RBF) {
-          float s, c;
-          rf_sincos(at[r], &s, &c);
-          da[r] = -(cl * s) * dpc[r] + (cl * c) * dps[r];
-        } else {
-          da[r] = at[r] > 0.f ? cl * dpc[r] : 0.f;
-        }
-      }
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt)
         if (dt < ND) {
-          // rows k >= dxw of the staged block are never written: they only feed discarded outputs
-          const f4 ox = *reinterpret_cast<const f4*>(osl + (dt * 16 + lr) * OST + wave * 16 + 4 * lq);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) dxa[dt] = mfma16(ox[r], da[r], dxa[dt]);
+          for (int r = 0; r < 4; ++r) dxa[dt] = mfma16(oxv[dt][r], da[r], dxa[dt]);
         }
     }
   }
@@ -869,37 +940,42 @@ LayerK make_layer_k(const dgprf_plan_t& pl, const StepDev& sd, int l, int& lds_f
            a.R % 4 == 0 && pl.ws_chain < (1 << 29);
   a.xmag = div_magic(dpad);
   a.dmag = div_magic(a.g);
+  a.n_rt = pl.n_row_tiles;
+  a.ns = pl.ns[l];
+  a.rt_per_xcd = (pl.n_row_tiles + 7) / 8;
   return a;
 }
 
 #define DGPRF_KS_NOT_DISPATCH(KERNEL)                                                              \
-  template <int KS, int NOT>                                                                       \
+  template <int KS, int NOT, bool G1>                                                              \
   void KERNEL##_launch3(bool rbf, dim3 grid, size_t lds, hipStream_t s, const LayerK& a) {         \
     if (rbf) {                                                                                     \
-      dgprf::set_lds_limit((const void*)KERNEL<KS, NOT, true>, lds);                               \
-      hipLaunchKernelGGL((KERNEL<KS, NOT, true>), grid, dim3(256), lds, s, a);                     \
+      dgprf::set_lds_limit((const void*)KERNEL<KS, NOT, true, G1>, lds);                           \
+      hipLaunchKernelGGL((KERNEL<KS, NOT, true, G1>), grid, dim3(256), lds, s, a);                 \
     } else {                                                                                       \
-      dgprf::set_lds_limit((const void*)KERNEL<KS, NOT, false>, lds);                              \
-      hipLaunchKernelGGL((KERNEL<KS, NOT, false>), grid, dim3(256), lds, s, a);                    \
+      dgprf::set_lds_limit((const void*)KERNEL<KS, NOT, false, G1>, lds);                          \
+      hipLaunchKernelGGL((KERNEL<KS, NOT, false, G1>), grid, dim3(256), lds, s, a);                \
     }                                                                                              \
   }                                                                                                \
   template <int KS>                                                                                \
-  void KERNEL##_launch2(int NOT, bool rbf, dim3 grid, size_t lds, hipStream_t s,                   \
+  void KERNEL##_launch2(int g, bool rbf, dim3 grid, size_t lds, hipStream_t s,                     \
                         const LayerK& a) {                                                         \
-    switch (NOT) {                                                                                 \
-      case 1: KERNEL##_launch3<KS, 1>(rbf, grid, lds, s, a); break;                                \
-      case 2: KERNEL##_launch3<KS, 2>(rbf, grid, lds, s, a); break;                                \
-      case 3: KERNEL##_launch3<KS, 3>(rbf, grid, lds, s, a); break;                                \
-      default: KERNEL##_launch3<KS, 4>(rbf, grid, lds, s, a); break;                               \
+    const int NOT = (g + 15) >> 4;                                                                 \
+    if (g == 1) KERNEL##_launch3<KS, 1, true>(rbf, grid, lds, s, a);                               \
+    else switch (NOT) {                                                                            \
+      case 1: KERNEL##_launch3<KS, 1, false>(rbf, grid, lds, s, a); break;                         \
+      case 2: KERNEL##_launch3<KS, 2, false>(rbf, grid, lds, s, a); break;                         \
+      case 3: KERNEL##_launch3<KS, 3, false>(rbf, grid, lds, s, a); break;                         \
+      default: KERNEL##_launch3<KS, 4, false>(rbf, grid, lds, s, a); break;                        \
     }                                                                                              \
   }                                                                                                \
-  void KERNEL##_launch(int d, int NOT, bool rbf, dim3 grid, size_t lds, hipStream_t s,             \
+  void KERNEL##_launch(int d, int g, bool rbf, dim3 grid, size_t lds, hipStream_t s,               \
                        const LayerK& a) {                                                          \
-    if (d <= 4) KERNEL##_launch2<1>(NOT, rbf, grid, lds, s, a);                                    \
-    else if (d <= 8) KERNEL##_launch2<2>(NOT, rbf, grid, lds, s, a);                               \
-    else if (d <= 16) KERNEL##_launch2<4>(NOT, rbf, grid, lds, s, a);                              \
-    else if (d <= 32) KERNEL##_launch2<8>(NOT, rbf, grid, lds, s, a);                              \
-    else KERNEL##_launch2<0>(NOT, rbf, grid, lds, s, a);                                           \
+    if (d <= 4) KERNEL##_launch2<1>(g, rbf, grid, lds, s, a);                                      \
+    else if (d <= 8) KERNEL##_launch2<2>(g, rbf, grid, lds, s, a);                                 \
+    else if (d <= 16) KERNEL##_launch2<4>(g, rbf, grid, lds, s, a);                                \
+    else if (d <= 32) KERNEL##_launch2<8>(g, rbf, grid, lds, s, a);                                \
+    else KERNEL##_launch2<0>(g, rbf, grid, lds, s, a);                                             \
   }
 
 DGPRF_KS_NOT_DISPATCH(k_step_fwd)
@@ -925,9 +1001,8 @@ namespace dgprf {
 hipError_t launch_step_fwd(const dgprf_plan_t& pl, const StepDev& sd, int layer, hipStream_t s) {
   int lds_floats = 0;
   const LayerK a = make_layer_k(pl, sd, layer, lds_floats);
-  dim3 grid(pl.n_row_tiles, pl.ns[layer], pl.n_chains);
-  const int NOT = (pl.n_gp[layer] + 15) >> 4;
-  k_step_fwd_launch(pl.d[layer], NOT, pl.kind[layer] == DGPRF_RBF, grid,
+  dim3 grid(8 * a.rt_per_xcd * a.ns, 1, pl.n_chains);
+  k_step_fwd_launch(pl.d[layer], pl.n_gp[layer], pl.kind[layer] == DGPRF_RBF, grid,
                     (size_t)lds_floats * sizeof(float), s, a);
   return hipGetLastError();
 }
@@ -935,9 +1010,8 @@ hipError_t launch_step_fwd(const dgprf_plan_t& pl, const StepDev& sd, int layer,
 hipError_t launch_step_bwd(const dgprf_plan_t& pl, const StepDev& sd, int layer, hipStream_t s) {
   int lds_floats = 0;
   const LayerK a = make_layer_k(pl, sd, layer, lds_floats);
-  dim3 grid(pl.n_row_tiles, pl.ns[layer], pl.n_chains);
-  const int NOT = (pl.n_gp[layer] + 15) >> 4;
-  k_step_bwd_launch(pl.d[layer], NOT, pl.kind[layer] == DGPRF_RBF, grid,
+  dim3 grid(8 * a.rt_per_xcd * a.ns, 1, pl.n_chains);
+  k_step_bwd_launch(pl.d[layer], pl.n_gp[layer], pl.kind[layer] == DGPRF_RBF, grid,
                     (size_t)lds_floats * sizeof(float), s, a);
   return hipGetLastError();
 }

@@ -51,8 +51,8 @@ for k in order:
     cyc = st[:, 14] - st[:, 0]
     freq = cyc / np.maximum(real_end - real0, 1) * 100e6
     segs = []
-    marks = [i for i in range(0, 8) if (st[:, i] > 0).all()] + [14]
-    if (st[:, 8] > 0).all():  # placement: HW_ID (simd [5:4], cu [11:8], sh [12], se [15:13]) | XCC << 32
+    marks = [i for i in range(0, 13) if (st[:, i] > 0).all()] + [14]
+    if False:  # placement (needs DGPRF_STAMP_HWID in the kernel): HW_ID (simd [5:4], cu [11:8], sh [12], se [15:13]) | XCC << 32
         hw = st[:, 8:12]
         simd = (hw >> 4) & 3
         cu_key = ((hw[:, 0] >> 32) << 16) | (((hw[:, 0] >> 13) & 7) << 8) | (((hw[:, 0] >> 12) & 1) << 4) | ((hw[:, 0] >> 8) & 15)
