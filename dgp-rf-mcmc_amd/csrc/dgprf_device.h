@@ -143,6 +143,11 @@ __host__ __device__ __forceinline__ uint32_t feistel_perm(uint32_t x, uint64_t n
 }
 
 // ---------------------------------------------------------------- trig
+#ifdef DGPRF_PRECISE_TRIG
+#define DGPRF_PRECISE_TRIG_ON true
+#else
+#define DGPRF_PRECISE_TRIG_ON false
+#endif
 // cos/sin of the RF inner products.  Range-reduce in revolutions (x/2pi - rint) and use the
 // hardware v_sin/v_cos (which take revolutions).  DGPRF_PRECISE_TRIG selects ocml sincosf.
 __device__ __forceinline__ void rf_sincos(float x, float* s, float* c) {

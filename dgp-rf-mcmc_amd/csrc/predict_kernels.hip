@@ -400,17 +400,18 @@ constexpr int TW_ROWS = NW * TR;  // rows per workgroup
 #define DGPRF_TILE_WAVES 4  // waves per SIMD the register budget must allow (latency hiding)
 #endif
 constexpr int TW_OST = 80;        // LDS row stride of a staged Omega block (conflict-free reads)
+__host__ __device__ constexpr int tw_wst(int notm) { return 16 * notm + 4; }  // W row stride
 
 struct TileLds {
   int obuf, wbuf, o_off, w_off, xin_off, xin_st, f_off, ftst, total;
 };
 
-__host__ __device__ inline TileLds tile_lds(const dgprf_plan_t& pl, int njw, int njo) {
+__host__ __device__ inline TileLds tile_lds(const dgprf_plan_t& pl, int notmax, int njo) {
   int gmax = 1;
   for (int l = 0; l < pl.n_layers; ++l) gmax = pl.n_gp[l] > gmax ? pl.n_gp[l] : gmax;
   TileLds T;
-  T.obuf = 16 * njo * TW_OST;                                  // njo float4 per thread: 16 rows each
-  T.wbuf = (2 * 64 * gmax > 1024 * njw) ? 2 * 64 * gmax : 1024 * njw;
+  T.obuf = 16 * njo * TW_OST;               // njo float4 per thread: 16 Omega rows each
+  T.wbuf = 2 * 64 * tw_wst(notmax);         // [cos|sin][64 features][16 NOT + 4]
   T.o_off = 0;
   T.w_off = 2 * T.obuf;
   T.xin_st = round4(pl.d_in);
@@ -421,29 +422,33 @@ __host__ __device__ inline TileLds tile_lds(const dgprf_plan_t& pl, int njw, int
   return T;
 }
 
-// One layer for the calling wave's 16 rows.  JW / JO: float4 W / Omega loads per thread per block.
-template <int NOT, bool RBF, bool G1, int JW, int JO>
+// One layer for the calling wave's 16 rows.
+//   JW / JO: float4 W / Omega loads per thread per 64-feature block; KS: k-steps of A = Omega^T x
+//   (>= ceil(d/4); extra k-steps multiply staged zeros).
+// Staged layouts: Omega [k][TW_OST] (x 1/2pi for the hardware sin/cos), W [h][feature][WST] with
+// WST = 16 NOT + 4 (g == 1: raw [h][64]); feature rows >= R are zeroed while staging, and output
+// columns o >= g are never stored, so the fragment reads need neither masks nor clamps and all
+// their offsets are immediates.
+template <int NOT, bool RBF, bool G1, int JW, int JO, int KS>
 __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
                                            const float* __restrict__ W,
                                            const float* __restrict__ om, float cl,
                                            const TileLds& T, float* smem, float* xin, float* ftw,
-                                           int wave, int lr, int lq, int64_t wrow0, int64_t n,
-                                           float* fout) {
+                                           int lr, int lq, int64_t wrow0, int64_t n, float* fout) {
+  constexpr int WST = tw_wst(NOT);
+  constexpr bool REV = RBF && !DGPRF_PRECISE_TRIG_ON;
   const int d = pl.d[layer], R = pl.n_rf[layer], g = pl.n_gp[layer];
   const int gp = layer > 0 ? pl.n_gp[layer - 1] : 0;
   const int tid = threadIdx.x;
+  const int gmag = (1048576 + g - 1) / g;  // floor(e / g) = (e * gmag) >> 20 for e < 4096
   // x fragments of the A = Omega^T x contraction: xf[ks] = X_l[row lr][4ks + lq]
-  float xf[8];
+  float xf[KS];
 #pragma unroll
-  for (int ks = 0; ks < 8; ++ks) {
+  for (int ks = 0; ks < KS; ++ks) {
     const int col = 4 * ks + lq;
-    float v = 0.f;
-    if (4 * ks < d) {
-      const float a = ftw[lr * T.ftst + min(col, T.ftst - 1)];
-      const float b = xin[lr * T.xin_st + min(max(col - gp, 0), T.xin_st - 1)];
-      v = col < gp ? a : (col < d ? b : 0.f);
-    }
-    xf[ks] = v;
+    const float a = ftw[lr * T.ftst + min(col, T.ftst - 1)];
+    const float b = xin[lr * T.xin_st + min(max(col - gp, 0), T.xin_st - 1)];
+    xf[ks] = col < gp ? a : (col < d ? b : 0.f);
   }
   const rsrc_t rw = make_rsrc(W, (int64_t)(RBF ? 2 : 1) * R * g);
   const rsrc_t ro = make_rsrc(om, (int64_t)d * R);
@@ -461,15 +466,37 @@ __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
       so[j] = bload4(ro, k < d && fb + 4 * c4 < R ? (uint32_t)((k * R + fb + 4 * c4) * 4) : DGPRF_OOB);
     }
   };
-  auto stage_store = [&](int buf) {
+  auto stage_store = [&](int buf, int fb) {
     float* wsb = smem + T.w_off + buf * T.wbuf;
     float* osb = smem + T.o_off + buf * T.obuf;
 #pragma unroll
-    for (int j = 0; j < JW; ++j) *reinterpret_cast<f4*>(wsb + 4 * (tid + 256 * j)) = sw[j];
+    for (int j = 0; j < JW; ++j) {
+      const int i = tid + 256 * j;
+      if (i < nwq) {
+        const int h = i >= 16 * g, e0 = 4 * (i - h * 16 * g);
+        if (G1) {  // raw [h][64]: rows e0..e0+3
+          f4 v = sw[j];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) v[t] = fb + e0 + t < R ? v[t] : 0.f;
+          *reinterpret_cast<f4*>(wsb + h * 64 + e0) = v;
+        } else if ((g & 3) == 0) {  // the float4 lies in one row
+          const int row = (e0 * gmag) >> 20, col = e0 - row * g;
+          const f4 v = fb + row < R ? sw[j] : f4zero();
+          *reinterpret_cast<f4*>(wsb + (h * 64 + row) * WST + col) = v;
+        } else {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const int e = e0 + t, row = (e * gmag) >> 20, col = e - row * g;
+            if (row < 64) wsb[(h * 64 + row) * WST + col] = fb + row < R ? sw[j][t] : 0.f;
+          }
+        }
+      }
+    }
 #pragma unroll
     for (int j = 0; j < JO; ++j) {
       const int i = tid + 256 * j;
-      *reinterpret_cast<f4*>(osb + (i >> 4) * TW_OST + 4 * (i & 15)) = so[j];
+      *reinterpret_cast<f4*>(osb + (i >> 4) * TW_OST + 4 * (i & 15)) =
+          REV ? so[j] * 0.15915494309189535f : so[j];
     }
   };
 
@@ -479,81 +506,78 @@ __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
   float dot = 0.f;
   const int nb = (R + 63) >> 6;
   stage_load(0);
-  stage_store(0);
+  stage_store(0, 0);
   __syncthreads();
   for (int blk = 0; blk < nb; ++blk) {
     const int fb = blk * 64, buf = blk & 1;
     if (blk + 1 < nb) stage_load(fb + 64);
     const float* wsb = smem + T.w_off + buf * T.wbuf;
-    const float* osb = smem + T.o_off + buf * T.obuf;
+    const float* osb = smem + T.o_off + buf * T.obuf + lq * TW_OST + lr;
+    const float* wl = wsb + (G1 ? 4 * lq : 4 * lq * WST + lr);
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       // A[row lr][feature fb + 16c + 4lq + r]
       f4 at = f4zero();
 #pragma unroll
-      for (int ks = 0; ks < 8; ++ks)
-        if (4 * ks < d) at = mfma16(osb[(4 * ks + lq) * TW_OST + 16 * c + lr], xf[ks], at);
+      for (int ks = 0; ks < KS; ++ks) at = mfma16(osb[4 * ks * TW_OST + 16 * c], xf[ks], at);
+      // features without the scale c (applied once to F): cos/sin(A) or relu(A)
       float p0[4], p1[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        if (RBF) {
+        if (REV) {
+          const float t = __builtin_amdgcn_fractf(at[r]);
+          p0[r] = __builtin_amdgcn_cosf(t);
+          p1[r] = __builtin_amdgcn_sinf(t);
+        } else if (RBF) {
           float sv, cv;
           rf_sincos(at[r], &sv, &cv);
-          p0[r] = cl * cv;
-          p1[r] = cl * sv;
+          p0[r] = cv;
+          p1[r] = sv;
         } else {
-          p0[r] = cl * fmaxf(at[r], 0.f);
+          p0[r] = fmaxf(at[r], 0.f);
           p1[r] = 0.f;
         }
       }
-      const int fl = 16 * c + 4 * lq;  // first feature of this lane within the block
       if (G1) {
-        const f4 w0 = *reinterpret_cast<const f4*>(wsb + fl);
-        const f4 w1 = RBF ? *reinterpret_cast<const f4*>(wsb + 64 + fl) : f4zero();
+        const f4 w0 = *reinterpret_cast<const f4*>(wl + 16 * c);
+        const f4 w1 = RBF ? *reinterpret_cast<const f4*>(wl + 64 + 16 * c) : f4zero();
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float m = fb + fl + r < R ? 1.f : 0.f;
-          dot = fmaf(p0[r], w0[r] * m, dot);
-          if (RBF) dot = fmaf(p1[r], w1[r] * m, dot);
+          dot = fmaf(p0[r], w0[r], dot);
+          if (RBF) dot = fmaf(p1[r], w1[r], dot);
         }
       } else {
 #pragma unroll
-        for (int ot = 0; ot < NOT; ++ot) {
-          const int o = ot * 16 + lr;
+        for (int ot = 0; ot < NOT; ++ot)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const bool ok = o < g && fb + fl + r < R;
-            const int wi = (fl + r) * g + min(o, g - 1);
-            const float w0 = ok ? wsb[wi] : 0.f;
-            acc[ot] = mfma16(w0, p0[r], acc[ot]);
-            if (RBF) {
-              const float w1 = ok ? wsb[64 * g + wi] : 0.f;
-              acs[ot] = mfma16(w1, p1[r], acs[ot]);
-            }
+            const int off = (16 * c + r) * WST + 16 * ot;
+            acc[ot] = mfma16(wl[off], p0[r], acc[ot]);
+            if (RBF) acs[ot] = mfma16(wl[64 * WST + off], p1[r], acs[ot]);
           }
-        }
       }
     }
-    if (blk + 1 < nb) stage_store(buf ^ 1);
+    if (blk + 1 < nb) stage_store(buf ^ 1, fb + 64);
     __syncthreads();
   }
   // F tile of this wave -> ftw (the next layer's input) and the optional per-layer output
   if (G1) {
     dot += __shfl_xor(dot, 16);
     dot += __shfl_xor(dot, 32);
+    dot *= cl;
     if (lq == 0) {
       ftw[lr * T.ftst] = dot;
       if (fout && wrow0 + lr < n) fout[wrow0 + lr] = dot;
     }
   } else {
-    // acc[ot][r] = F[row lr][ot*16 + 4lq + r]
+    // acc[ot][r] = F[row lr][ot*16 + 4lq + r] / c
 #pragma unroll
     for (int ot = 0; ot < NOT; ++ot)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int o = ot * 16 + 4 * lq + r;
         if (o < g) {
-          const float v = acc[ot][r] + acs[ot][r];
+          const float v = cl * (acc[ot][r] + acs[ot][r]);
           ftw[lr * T.ftst + o] = v;
           if (fout && wrow0 + lr < n) fout[(wrow0 + lr) * g + o] = v;
         }
@@ -571,7 +595,7 @@ void k_forward_tiles(
     float* __restrict__ se_out, float* __restrict__ lse_m, float* __restrict__ lse_s,
     float* __restrict__ se_sum) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const TileLds T = tile_lds(pl, JW, JO);
+  const TileLds T = tile_lds(pl, NOTMAX, JO);
   const int chain = blockIdx.y;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, lr = lane & 15, lq = lane >> 4;
   const int64_t wrow0 = (int64_t)blockIdx.x * TW_ROWS + wave * TR;
@@ -592,11 +616,17 @@ void k_forward_tiles(
     const float* __restrict__ W = Wc + pl.w_off[layer];
     const float cl = der[layer];
     const int g = pl.n_gp[layer], NOT = (g + 15) >> 4;
-    const bool rbf = pl.kind[layer] == DGPRF_RBF;
+    const bool rbf = pl.kind[layer] == DGPRF_RBF, ks2 = pl.d[layer] <= 8;
     float* fout = fo.p[layer] ? fo.p[layer] + (int64_t)chain * n * g : nullptr;
-#define DGPRF_TL(NT, RB, G1_)                                                                  \
-  tile_layer<NT, RB, G1_, JW, JO>(pl, layer, W, om, cl, T, smem, xin, ftw, wave, lr, lq, wrow0, n, \
-                              fout)
+#define DGPRF_TL(NT, RB, G1_)                                                                       \
+  do {                                                                                              \
+    if (ks2)                                                                                        \
+      tile_layer<NT, RB, G1_, JW, JO, 2>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, n, \
+                                         fout);                                                     \
+    else                                                                                            \
+      tile_layer<NT, RB, G1_, JW, JO, 8>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, n, \
+                                         fout);                                                     \
+  } while (0)
     if (g == 1) {
       if (rbf) DGPRF_TL(1, true, true);
       else DGPRF_TL(1, false, true);
@@ -685,7 +715,8 @@ hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const
     // >= 16 d / 256; the wide-g instances are compiled with JO = 2 only (host and kernel must size
     // the LDS ring identically)
     const int njo = (dmax <= 16 && njw <= 2) ? 1 : 2;
-    const TileLds T = tile_lds(pl, njw, njo);
+    const int ntm = njw <= 2 ? 1 : (njw == 4 ? 2 : 4);
+    const TileLds T = tile_lds(pl, ntm, njo);
     dim3 tgrid((unsigned)((n + TW_ROWS - 1) / TW_ROWS), pl.n_chains);
     const size_t tl = (size_t)T.total * sizeof(float);
 #define DGPRF_TILE_LAUNCH(NM, J, JO)                                                               \

@@ -1,0 +1,40 @@
+"""Profiling driver: predictive forward of the config-2 model on the 1e5-row test set.
+
+  rocprofv3 --kernel-trace --stats -d gpurun_out/prof_pred -o run --output-format csv -- \
+      python3 scripts/prof_predict.py --samples 20
+  rocprofv3 --pmc SQ_WAVE_CYCLES ... --output-format csv -d ... -- python3 scripts/prof_predict.py
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "dgp-rf-mcmc_amd")]
+
+from dgprf import engine as E  # noqa: E402
+from dgprf.data import regression_data  # noqa: E402
+from dgprf.predictive import PredictiveLSE  # noqa: E402
+from likelihoods import Gaussian  # noqa: E402
+from models.regression_model import RegressionDGP  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--samples", type=int, default=10)
+ap.add_argument("--n-test", type=int, default=100_000)
+args = ap.parse_args()
+dev = torch.device("cuda", 0)
+_, _, a = regression_data(1000, 8, seed=0, device=dev)
+Xt, Yt, _ = regression_data(args.n_test, 8, seed=1, device=dev, a=a)
+E.set_seed(2)
+m = RegressionDGP(8, 1, n_hidden_layers=3, n_rf=1024, n_gp=[8, 8, 1], likelihood=Gaussian(variance=0.1))
+m.precond_update(None, 1_000_000, precond_type="identity")
+acc = PredictiveLSE(m._engine, Xt, Yt)
+acc.add_sample()
+ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+ev0.record()
+for _ in range(args.samples):
+    acc.add_sample(build=False)
+ev1.record()
+torch.cuda.synchronize()
+print(f"predictive: {ev0.elapsed_time(ev1) / args.samples * 1e3:.1f} us/sample")
