@@ -332,10 +332,10 @@ int dgprf_profile_step(const dgprf_plan_t* plan, const dgprf_chain_t* chain,
   st.grad_only = 0;
   const UpdateDev ud = make_update_dev(st);
   const int L = plan->n_layers, K = 2 * L + 1;
-  hipEvent_t ev[2 * (2 * DGPRF_MAX_LAYERS + 1)] = {};
+  hipEvent_t ev[2 * (2 * DGPRF_MAX_LAYERS + 2)] = {};
   hipError_t e = hipSuccess;
-  for (int i = 0; i < 2 * K && e == hipSuccess; ++i) e = hipEventCreate(&ev[i]);
-  for (int k = 0; k < K; ++k) ms_out[k] = 0.f;
+  for (int i = 0; i < 2 * (K + 1) && e == hipSuccess; ++i) e = hipEventCreate(&ev[i]);
+  for (int k = 0; k <= K; ++k) ms_out[k] = 0.f;
   // the real step sequence (fwd 0..L-1, bwd L-1..0, update), every kernel between two events
   for (int rep = 0; rep < reps && e == hipSuccess; ++rep) {
     const StepDev sd = make_step_dev(*plan, *chain, *batch, st.step_offset);
@@ -350,14 +350,16 @@ int dgprf_profile_step(const dgprf_plan_t* plan, const dgprf_chain_t* chain,
       if (e == hipSuccess) e = hipEventRecord(ev[2 * kk + 1], s);
     }
     if (e == hipSuccess) e = dgprf::launch_advance(chain->step, 1, s);
-    if (e == hipSuccess) e = hipEventSynchronize(ev[2 * (2 * L) + 1]);
-    for (int kk = 0; kk < K && e == hipSuccess; ++kk) {
+    if (e == hipSuccess) e = hipEventRecord(ev[2 * K], s);  // empty pair: the pair's own cost
+    if (e == hipSuccess) e = hipEventRecord(ev[2 * K + 1], s);
+    if (e == hipSuccess) e = hipEventSynchronize(ev[2 * K + 1]);
+    for (int kk = 0; kk <= K && e == hipSuccess; ++kk) {
       float ms = 0.f;
       e = hipEventElapsedTime(&ms, ev[2 * kk], ev[2 * kk + 1]);
       ms_out[kk] += ms / (float)reps;
     }
   }
-  for (int i = 0; i < 2 * K; ++i)
+  for (int i = 0; i < 2 * (K + 1); ++i)
     if (ev[i]) (void)hipEventDestroy(ev[i]);
   return hip_rc(e);
 }

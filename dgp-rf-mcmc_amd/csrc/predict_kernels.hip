@@ -399,6 +399,9 @@ constexpr int TW_ROWS = NW * TR;  // rows per workgroup
 #ifndef DGPRF_TILE_WAVES
 #define DGPRF_TILE_WAVES 4  // waves per SIMD the register budget must allow (latency hiding)
 #endif
+#ifndef DGPRF_TILE_TPW_DEFAULT
+#define DGPRF_TILE_TPW_DEFAULT 1  // 16-row tiles per wave (2: two chains per wave, but 186 VGPRs -> 2 waves/SIMD, slower)
+#endif
 constexpr int TW_OST = 80;        // LDS row stride of a staged Omega block (conflict-free reads)
 __host__ __device__ constexpr int tw_wst(int notm) { return 16 * notm + 4; }  // W row stride
 
@@ -406,7 +409,7 @@ struct TileLds {
   int obuf, wbuf, o_off, w_off, xin_off, xin_st, f_off, ftst, total;
 };
 
-__host__ __device__ inline TileLds tile_lds(const dgprf_plan_t& pl, int notmax, int njo) {
+__host__ __device__ inline TileLds tile_lds(const dgprf_plan_t& pl, int notmax, int njo, int tpw) {
   int gmax = 1;
   for (int l = 0; l < pl.n_layers; ++l) gmax = pl.n_gp[l] > gmax ? pl.n_gp[l] : gmax;
   TileLds T;
@@ -417,8 +420,8 @@ __host__ __device__ inline TileLds tile_lds(const dgprf_plan_t& pl, int notmax, 
   T.xin_st = round4(pl.d_in);
   T.xin_off = T.w_off + 2 * T.wbuf;
   T.ftst = gmax + 1;
-  T.f_off = T.xin_off + NW * TR * T.xin_st;
-  T.total = T.f_off + NW * round4(TR * T.ftst);
+  T.f_off = T.xin_off + NW * tpw * TR * T.xin_st;
+  T.total = T.f_off + NW * round4(tpw * TR * T.ftst);
   return T;
 }
 
@@ -429,7 +432,7 @@ __host__ __device__ inline TileLds tile_lds(const dgprf_plan_t& pl, int notmax, 
 // WST = 16 NOT + 4 (g == 1: raw [h][64]); feature rows >= R are zeroed while staging, and output
 // columns o >= g are never stored, so the fragment reads need neither masks nor clamps and all
 // their offsets are immediates.
-template <int NOT, bool RBF, bool G1, int JW, int JO, int KS>
+template <int NOT, bool RBF, bool G1, int JW, int JO, int KS, int TPW>
 __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
                                            const float* __restrict__ W,
                                            const float* __restrict__ om, float cl,
@@ -441,15 +444,17 @@ __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
   const int gp = layer > 0 ? pl.n_gp[layer - 1] : 0;
   const int tid = threadIdx.x;
   const int gmag = (1048576 + g - 1) / g;  // floor(e / g) = (e * gmag) >> 20 for e < 4096
-  // x fragments of the A = Omega^T x contraction: xf[ks] = X_l[row lr][4ks + lq]
-  float xf[KS];
+  // x fragments of the A = Omega^T x contraction: xf[t][ks] = X_l[tile t, row lr][4ks + lq]
+  float xf[TPW][KS];
 #pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    const int col = 4 * ks + lq;
-    const float a = ftw[lr * T.ftst + min(col, T.ftst - 1)];
-    const float b = xin[lr * T.xin_st + min(max(col - gp, 0), T.xin_st - 1)];
-    xf[ks] = col < gp ? a : (col < d ? b : 0.f);
-  }
+  for (int t = 0; t < TPW; ++t)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int col = 4 * ks + lq, row = t * TR + lr;
+      const float a = ftw[row * T.ftst + min(col, T.ftst - 1)];
+      const float b = xin[row * T.xin_st + min(max(col - gp, 0), T.xin_st - 1)];
+      xf[t][ks] = col < gp ? a : (col < d ? b : 0.f);
+    }
   const rsrc_t rw = make_rsrc(W, (int64_t)(RBF ? 2 : 1) * R * g);
   const rsrc_t ro = make_rsrc(om, (int64_t)d * R);
   const int nwq = (RBF ? 32 : 16) * g;  // float4 of one W block
@@ -500,10 +505,14 @@ __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
     }
   };
 
-  f4 acc[NOT], acs[NOT];
+  f4 acc[TPW][NOT], acs[TPW][NOT];
+  float dot[TPW];
 #pragma unroll
-  for (int ot = 0; ot < NOT; ++ot) acc[ot] = acs[ot] = f4zero();
-  float dot = 0.f;
+  for (int t = 0; t < TPW; ++t) {
+    dot[t] = 0.f;
+#pragma unroll
+    for (int ot = 0; ot < NOT; ++ot) acc[t][ot] = acs[t][ot] = f4zero();
+  }
   const int nb = (R + 63) >> 6;
   stage_load(0);
   stage_store(0, 0);
@@ -516,78 +525,100 @@ __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
     const float* wl = wsb + (G1 ? 4 * lq : 4 * lq * WST + lr);
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      // A[row lr][feature fb + 16c + 4lq + r]
-      f4 at = f4zero();
+      // A[tile t, row lr][feature fb + 16c + 4lq + r]; the Omega / W fragments serve every tile
+      float om[KS];
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) at = mfma16(osb[4 * ks * TW_OST + 16 * c], xf[ks], at);
-      // features without the scale c (applied once to F): cos/sin(A) or relu(A)
-      float p0[4], p1[4];
+      for (int ks = 0; ks < KS; ++ks) om[ks] = osb[4 * ks * TW_OST + 16 * c];
+      f4 at[TPW];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (REV) {
-          const float t = __builtin_amdgcn_fractf(at[r]);
-          p0[r] = __builtin_amdgcn_cosf(t);
-          p1[r] = __builtin_amdgcn_sinf(t);
-        } else if (RBF) {
-          float sv, cv;
-          rf_sincos(at[r], &sv, &cv);
-          p0[r] = cv;
-          p1[r] = sv;
-        } else {
-          p0[r] = fmaxf(at[r], 0.f);
-          p1[r] = 0.f;
-        }
+      for (int t = 0; t < TPW; ++t) {
+        at[t] = f4zero();
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) at[t] = mfma16(om[ks], xf[t][ks], at[t]);
       }
+      // features without the scale c (applied once to F): cos/sin(A) or relu(A)
+      float p0[TPW][4], p1[TPW][4];
+#pragma unroll
+      for (int t = 0; t < TPW; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if (REV) {
+            const float u = __builtin_amdgcn_fractf(at[t][r]);
+            p0[t][r] = __builtin_amdgcn_cosf(u);
+            p1[t][r] = __builtin_amdgcn_sinf(u);
+          } else if (RBF) {
+            float sv, cv;
+            rf_sincos(at[t][r], &sv, &cv);
+            p0[t][r] = cv;
+            p1[t][r] = sv;
+          } else {
+            p0[t][r] = fmaxf(at[t][r], 0.f);
+            p1[t][r] = 0.f;
+          }
+        }
       if (G1) {
         const f4 w0 = *reinterpret_cast<const f4*>(wl + 16 * c);
         const f4 w1 = RBF ? *reinterpret_cast<const f4*>(wl + 64 + 16 * c) : f4zero();
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          dot = fmaf(p0[r], w0[r], dot);
-          if (RBF) dot = fmaf(p1[r], w1[r], dot);
-        }
+        for (int t = 0; t < TPW; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            dot[t] = fmaf(p0[t][r], w0[r], dot[t]);
+            if (RBF) dot[t] = fmaf(p1[t][r], w1[r], dot[t]);
+          }
       } else {
 #pragma unroll
         for (int ot = 0; ot < NOT; ++ot)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int off = (16 * c + r) * WST + 16 * ot;
-            acc[ot] = mfma16(wl[off], p0[r], acc[ot]);
-            if (RBF) acs[ot] = mfma16(wl[64 * WST + off], p1[r], acs[ot]);
+            const float w0 = wl[off];
+            const float w1 = RBF ? wl[64 * WST + off] : 0.f;
+#pragma unroll
+            for (int t = 0; t < TPW; ++t) {
+              acc[t][ot] = mfma16(w0, p0[t][r], acc[t][ot]);
+              if (RBF) acs[t][ot] = mfma16(w1, p1[t][r], acs[t][ot]);
+            }
           }
       }
     }
     if (blk + 1 < nb) stage_store(buf ^ 1, fb + 64);
     __syncthreads();
   }
-  // F tile of this wave -> ftw (the next layer's input) and the optional per-layer output
-  if (G1) {
-    dot += __shfl_xor(dot, 16);
-    dot += __shfl_xor(dot, 32);
-    dot *= cl;
-    if (lq == 0) {
-      ftw[lr * T.ftst] = dot;
-      if (fout && wrow0 + lr < n) fout[wrow0 + lr] = dot;
-    }
-  } else {
-    // acc[ot][r] = F[row lr][ot*16 + 4lq + r] / c
+  // F tiles of this wave -> ftw (the next layer's input) and the optional per-layer output
 #pragma unroll
-    for (int ot = 0; ot < NOT; ++ot)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int o = ot * 16 + 4 * lq + r;
-        if (o < g) {
-          const float v = cl * (acc[ot][r] + acs[ot][r]);
-          ftw[lr * T.ftst + o] = v;
-          if (fout && wrow0 + lr < n) fout[(wrow0 + lr) * g + o] = v;
-        }
+  for (int t = 0; t < TPW; ++t) {
+    const int row = t * TR + lr;
+    const int64_t b = wrow0 + row;
+    if (G1) {
+      float v = dot[t];
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      v *= cl;
+      if (lq == 0) {
+        ftw[row * T.ftst] = v;
+        if (fout && b < n) fout[b] = v;
       }
+    } else {
+      // acc[t][ot][r] = F[tile t, row lr][ot*16 + 4lq + r] / c
+#pragma unroll
+      for (int ot = 0; ot < NOT; ++ot)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int o = ot * 16 + 4 * lq + r;
+          if (o < g) {
+            const float v = cl * (acc[t][ot][r] + acs[t][ot][r]);
+            ftw[row * T.ftst + o] = v;
+            if (fout && b < n) fout[b * g + o] = v;
+          }
+        }
+    }
   }
   __syncthreads();  // ftw complete before the next layer reads its x fragments
 }
 
-template <int NOTMAX, int JW, int JO>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DGPRF_TILE_WAVES)))
+template <int NOTMAX, int JW, int JO, int TPW>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? DGPRF_TILE_WAVES : 2)))
 void k_forward_tiles(
     const dgprf_plan_t pl, const float* __restrict__ theta, const float* __restrict__ omega,
     const float* __restrict__ der, const float* __restrict__ X, const float* __restrict__ Y,
@@ -595,21 +626,21 @@ void k_forward_tiles(
     float* __restrict__ se_out, float* __restrict__ lse_m, float* __restrict__ lse_s,
     float* __restrict__ se_sum) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const TileLds T = tile_lds(pl, NOTMAX, JO);
+  const TileLds T = tile_lds(pl, NOTMAX, JO, TPW);
   const int chain = blockIdx.y;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, lr = lane & 15, lq = lane >> 4;
-  const int64_t wrow0 = (int64_t)blockIdx.x * TW_ROWS + wave * TR;
-  float* xin = smem + T.xin_off + wave * TR * T.xin_st;
-  float* ftw = smem + T.f_off + wave * round4(TR * T.ftst);
+  const int64_t wrow0 = (int64_t)blockIdx.x * TW_ROWS * TPW + wave * TR * TPW;
+  float* xin = smem + T.xin_off + wave * TPW * TR * T.xin_st;
+  float* ftw = smem + T.f_off + wave * round4(TPW * TR * T.ftst);
   const float* Wc = theta + (int64_t)chain * pl.w_total;
   const int L = pl.n_layers;
   // this wave's X rows (zero past n)
-  for (int e = lane; e < TR * T.xin_st; e += 64) {
+  for (int e = lane; e < TPW * TR * T.xin_st; e += 64) {
     const int r = e / T.xin_st, k = e - r * T.xin_st;
     const int64_t b = wrow0 + r;
     xin[e] = (b < n && k < pl.d_in) ? X[b * pl.d_in + k] : 0.f;
   }
-  for (int e = lane; e < TR * T.ftst; e += 64) ftw[e] = 0.f;
+  for (int e = lane; e < TPW * TR * T.ftst; e += 64) ftw[e] = 0.f;
   __syncthreads();
   for (int layer = 0; layer < L; ++layer) {
     const float* __restrict__ om = omega + pl.omega_off[layer];
@@ -621,10 +652,10 @@ void k_forward_tiles(
 #define DGPRF_TL(NT, RB, G1_)                                                                       \
   do {                                                                                              \
     if (ks2)                                                                                        \
-      tile_layer<NT, RB, G1_, JW, JO, 2>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, n, \
+      tile_layer<NT, RB, G1_, JW, JO, 2, TPW>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, n, \
                                          fout);                                                     \
     else                                                                                            \
-      tile_layer<NT, RB, G1_, JW, JO, 8>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, n, \
+      tile_layer<NT, RB, G1_, JW, JO, 8, TPW>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, n, \
                                          fout);                                                     \
   } while (0)
     if (g == 1) {
@@ -642,13 +673,13 @@ void k_forward_tiles(
     }
 #undef DGPRF_TL
   }
-  // likelihood per row: lanes 0..15 of each wave, row lr of the wave's tile
+  // likelihood per row: lanes 0..15 of each wave, row lr of each of the wave's tiles
   const bool want_lik = logp_out || se_out || lse_m;
-  if (want_lik && lq == 0) {
-    const int64_t b = wrow0 + lr;
-    if (b < n) {
+  for (int t = 0; t < TPW; ++t) {
+    const int64_t b = wrow0 + t * TR + lr;
+    if (want_lik && lq == 0 && b < n) {
       const int g = pl.n_gp[L - 1];
-      const float* f = ftw + lr * T.ftst;
+      const float* f = ftw + (t * TR + lr) * T.ftst;
       const float* y = Y + b * y_cols;
       float lp = 0.f, se = 0.f;
       if (pl.likelihood == DGPRF_LIK_GAUSSIAN) {
@@ -716,14 +747,22 @@ hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const
     // the LDS ring identically)
     const int njo = (dmax <= 16 && njw <= 2) ? 1 : 2;
     const int ntm = njw <= 2 ? 1 : (njw == 4 ? 2 : 4);
-    const TileLds T = tile_lds(pl, ntm, njo);
-    dim3 tgrid((unsigned)((n + TW_ROWS - 1) / TW_ROWS), pl.n_chains);
-    const size_t tl = (size_t)T.total * sizeof(float);
+    const int tpw = getenv("DGPRF_TILE_TPW") ? atoi(getenv("DGPRF_TILE_TPW")) == 2 ? 2 : 1 : DGPRF_TILE_TPW_DEFAULT;
+    const TileLds T = tile_lds(pl, ntm, njo, tpw);
+    dim3 tgrid((unsigned)((n + TW_ROWS * tpw - 1) / (TW_ROWS * tpw)), pl.n_chains);
+    size_t tl = (size_t)T.total * sizeof(float);
+    if (const char* pad = getenv("DGPRF_TILE_LDS_BYTES")) tl = max(tl, (size_t)atol(pad));  // experiments
 #define DGPRF_TILE_LAUNCH(NM, J, JO)                                                               \
   do {                                                                                             \
-    set_lds_limit((const void*)k_forward_tiles<NM, J, JO>, tl);                                    \
-    hipLaunchKernelGGL((k_forward_tiles<NM, J, JO>), tgrid, dim3(256), tl, s, pl, theta, omega,    \
-                       der, X, Y, y_cols, n, fo, logp, se, lse_m, lse_s, se_sum);                  \
+    if (tpw == 2) {                                                                                \
+      set_lds_limit((const void*)k_forward_tiles<NM, J, JO, 2>, tl);                               \
+      hipLaunchKernelGGL((k_forward_tiles<NM, J, JO, 2>), tgrid, dim3(256), tl, s, pl, theta,      \
+                         omega, der, X, Y, y_cols, n, fo, logp, se, lse_m, lse_s, se_sum);         \
+    } else {                                                                                       \
+      set_lds_limit((const void*)k_forward_tiles<NM, J, JO, 1>, tl);                               \
+      hipLaunchKernelGGL((k_forward_tiles<NM, J, JO, 1>), tgrid, dim3(256), tl, s, pl, theta,      \
+                         omega, der, X, Y, y_cols, n, fo, logp, se, lse_m, lse_s, se_sum);         \
+    }                                                                                              \
   } while (0)
     if (njw == 1) {
       if (njo == 1) DGPRF_TILE_LAUNCH(1, 1, 1);

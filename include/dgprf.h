@@ -210,8 +210,9 @@ int dgprf_graph_destroy(dgprf_graph_handle graph);
 
 /* Per-kernel device time of the step sequence, measured with hipEvents on `stream`: `reps` real
  * steps (forward l = 0..L-1, backward L-1..0, update; the chain advances) with an event pair around
- * every kernel.  ms_out[k] receives the mean milliseconds of kernel k, indexed forward l -> l,
- * backward l -> L + l, update -> 2L. */
+ * every kernel.  ms_out[k] (2L + 2 entries) receives the mean milliseconds of the pair around kernel
+ * k, indexed forward l -> l, backward l -> L + l, update -> 2L, and ms_out[2L + 1] the mean of an
+ * empty pair recorded the same way (the pair's own cost, to subtract). */
 int dgprf_profile_step(const dgprf_plan_t *plan, const dgprf_chain_t *chain,
                        const dgprf_batch_t *batch, const dgprf_step_t *step, int32_t reps,
                        float *ms_out, void *stream);
