@@ -175,6 +175,82 @@ def grad_W(p, X, Y, N):
     return grads
 
 
+# ----------------------------------------------------------------------------- full Bayes
+class Trainable:
+    """Which hyper-parameters are tf.Variables with trainable=True in the reference:
+    kernel log_amplitude / log_inv_length_scale (kernel_trainable, models/dgp.py:58-73,
+    kernels/RBF.py:39-41), the layer means (set_nonzero_mean, layers/rf_layers.py:23-26) and the
+    Gaussian lik_log_var (likelihoods/gaussian.py:12); `ard[l]` False = one scalar length scale
+    for layer l (all d slots equal, gradient summed over them)."""
+
+    def __init__(self, kernel=True, lik=True, mean=False, ard=None):
+        self.kernel, self.lik, self.mean, self.ard = kernel, lik, mean, ard
+
+
+def U_full(p, X, Y, N, tr):
+    """Minibatch potential, full_bayesian=True — models/dgp.py:175-181: the N(0,1) prior over every
+    trainable variable (W, kernel hyper-parameters, means, lik_log_var) divided by N."""
+    B = X.shape[0]
+    lg = lambda v: np.sum(-0.5 * (LOG_2PI + np.asarray(v) ** 2))
+    pri = prior_W(p)
+    for l in range(p.L):
+        if tr.kernel:
+            pri += lg(p.log_amp[l])
+            ard = tr.ard is None or tr.ard[l]
+            pri += lg(p.log_inv_ls[l] if ard else p.log_inv_ls[l][:1])
+        if tr.mean:
+            pri += lg(p.mean[l])
+    if tr.lik and p.likelihood == "gaussian":
+        pri += lg(p.lik_log_var)
+    return -(pri / N + np.sum(log_prob(p, forward(p, X), Y)) / B)
+
+
+def grad_full(p, X, Y, N, tr):
+    """dU/d(every trainable variable), full_bayesian=True — the analytic form of tape.gradient
+    over self.trainable_variables (models/dgp.py:199-204).  Per layer (all layers):
+      gW = Phi^T dF + W/N,  dPhi = dF W^T,  g_log_amp = sum(dPhi * Phi) + log_amp/N
+      dA as in grad_W,  G = X_l^T dA  (dU/dOmega),  Omega = exp(lis) z + mean:
+      g_lis[k] = exp(lis[k]) sum_f G[k,f] z[k,f] + lis[k]/N   (scalar lis: summed over k)
+      g_mean[k] = sum_f G[k,f] + mean[k]/N
+    and g_lik_log_var = (1/B) sum_b sum_o (1 - (y-F)^2/var)/2 + lik_log_var/N (Gaussian).
+    Returns a dict of per-layer lists (+ 'lik_log_var'); entries of non-trainable groups are None.
+    """
+    X = np.asarray(X, dtype=p.dtype)
+    B = X.shape[0]
+    F, cache = forward(p, X, keep=True)
+    dF = -dlogp_dF(p, F, Y) / B
+    out = {"W": [None] * p.L, "log_amp": [None] * p.L, "log_inv_ls": [None] * p.L,
+           "mean": [None] * p.L, "lik_log_var": None}
+    for l in reversed(range(p.L)):
+        Xin, A, Phi, _ = cache[l]
+        out["W"][l] = Phi.T @ dF + p.W[l] / N
+        dPhi = dF @ p.W[l].T
+        c = amp_scale(p, l)
+        R = p.n_rf[l]
+        if tr.kernel:
+            out["log_amp"][l] = np.sum(dPhi * Phi) + p.log_amp[l] / N
+        if p.kinds[l] == "RBF":
+            dA = c * (-np.sin(A) * dPhi[:, :R] + np.cos(A) * dPhi[:, R:])
+        else:
+            dA = c * (A > 0) * dPhi
+        G = Xin.T @ dA
+        if tr.kernel:
+            g = np.exp(p.log_inv_ls[l]) * np.sum(G * p.z[l], axis=1)
+            ard = tr.ard is None or tr.ard[l]
+            if ard:
+                out["log_inv_ls"][l] = g + p.log_inv_ls[l] / N
+            else:
+                out["log_inv_ls"][l] = np.sum(g) + p.log_inv_ls[l][0] / N
+        if tr.mean:
+            out["mean"][l] = np.sum(G, axis=1) + p.mean[l] / N
+        if l > 0:
+            dF = (dA @ omega(p, l).T)[:, :p.n_gp[l - 1]]
+    if tr.lik and p.likelihood == "gaussian":
+        var = np.exp(p.lik_log_var)
+        out["lik_log_var"] = np.sum(0.5 * (1.0 - (Y - F) ** 2 / var)) / B + p.lik_log_var / N
+    return out
+
+
 # ----------------------------------------------------------------------------- update
 def sghmc_update(W, m, g, lr, N, beta, T, M, xi, xi_resample=None):
     """One SGHMC/SGLD update of one parameter tensor — models/dgp.py:206-216.
@@ -200,6 +276,58 @@ def sgmcmc_step(p, m_list, X, Y, N, lr, beta, T, M_list, xi_list, xi_resample_li
                                      xi_list[l], xr)
         out_m.append(m_new)
     return out_m
+
+
+def full_groups(p, tr):
+    """The trainable variables of full_bayesian=True in a fixed order, as (name, layer) keys:
+    per layer W, log_amp, log_inv_ls, mean (when trainable), then lik_log_var."""
+    keys = []
+    for l in range(p.L):
+        keys.append(("W", l))
+        if tr.kernel:
+            keys += [("log_amp", l), ("log_inv_ls", l)]
+        if tr.mean:
+            keys.append(("mean", l))
+    if tr.lik and p.likelihood == "gaussian":
+        keys.append(("lik_log_var", None))
+    return keys
+
+
+def get_var(p, key, tr):
+    name, l = key
+    if name == "lik_log_var":
+        return np.asarray(p.lik_log_var)
+    v = getattr(p, name)[l]
+    if name == "log_inv_ls" and tr.ard is not None and not tr.ard[l]:
+        return np.asarray(v[0])
+    return np.asarray(v)
+
+
+def set_var(p, key, tr, value):
+    name, l = key
+    if name == "lik_log_var":
+        p.lik_log_var = np.asarray(value, dtype=p.dtype)
+        return
+    if name == "log_inv_ls" and tr.ard is not None and not tr.ard[l]:
+        p.log_inv_ls[l] = np.full(p.d[l], value, dtype=p.dtype)
+        return
+    getattr(p, name)[l] = np.asarray(value, dtype=p.dtype)
+
+
+def sgmcmc_step_full(p, mom, X, Y, N, lr, beta, T, M, xi, tr, xi_resample=None):
+    """DGP_RF.sgmcmc_update(full_bayesian=True) with injected noise (models/dgp.py:199-216): every
+    trainable variable takes the same SGHMC update with its own momentum `mom[key]`, mass
+    `M[key]` and noise `xi[key]` (gradients all taken at the pre-update state)."""
+    g = grad_full(p, X, Y, N, tr)
+    new_mom = {}
+    for key in full_groups(p, tr):
+        name, l = key
+        gk = g[name] if name == "lik_log_var" else g[name][l]
+        xr = None if xi_resample is None else xi_resample[key]
+        v, m = sghmc_update(get_var(p, key, tr), mom[key], gk, lr, N, beta, T, M[key], xi[key], xr)
+        set_var(p, key, tr, v)
+        new_mom[key] = m
+    return new_mom
 
 
 # ----------------------------------------------------------------------------- preconditioner
