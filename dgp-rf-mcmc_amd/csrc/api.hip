@@ -37,7 +37,15 @@ StepDev make_step_dev(const dgprf_plan_t& pl, const dgprf_chain_t& ch, const dgp
   sd.bd.y_cols = b.y_cols;
   sd.bd.mode = b.mode;
   sd.step_offset = step_offset;
-  (void)pl;
+  sd.full_bayes = 0;
+  const bool pc = pl.hyp_per_chain != 0;
+  sd.om_cs = pc ? pl.omega_total : 0;
+  sd.der_cs = pc ? pl.der_total : 0;
+  sd.hyp_cs = pc ? pl.hyp_total : 0;
+  sd.z = ch.z;
+  sd.hyp = ch.hyp;
+  sd.hmom = ch.hmom;
+  sd.hmass = ch.hmass;
   return sd;
 }
 
@@ -55,6 +63,8 @@ UpdateDev make_update_dev(const dgprf_step_t& st) {
   ud.cycle_length = st.cycle_length > 0 ? st.cycle_length : 1;
   ud.xi = st.xi;
   ud.xi_resample = st.xi_resample;
+  ud.xi_hyp = st.xi_hyp;
+  ud.xi_hyp_resample = st.xi_hyp_resample;
   return ud;
 }
 
@@ -105,7 +115,16 @@ hipError_t enqueue_step(const dgprf_plan_t& pl, const StepDev& sd, const UpdateD
   for (int l = pl.n_layers - 1; l >= 0 && e == hipSuccess; --l)
     e = dgprf::launch_step_bwd(pl, sd, l, s);
   if (e == hipSuccess) e = dgprf::launch_step_update(pl, sd, ud, nullptr, s, gather_next);
+  if (e == hipSuccess && sd.full_bayes) e = dgprf::launch_step_hyper(pl, sd, ud, s);
   return e;
+}
+
+// full_bayesian=True needs the hyper-parameter state, and per-chain hyper-parameters when several
+// chains step at once
+int check_full_bayes(const dgprf_plan_t& pl, const dgprf_chain_t& ch) {
+  if (!ch.z || !ch.hyp || !ch.hmom || !ch.hmass) return DGPRF_E_ARG;
+  if (pl.n_chains > 1 && !pl.hyp_per_chain) return DGPRF_E_ARG;
+  return DGPRF_OK;
 }
 
 }  // namespace
@@ -141,17 +160,23 @@ int dgprf_plan_init(dgprf_plan_t* pl) {
     if (pl->kind[l] != DGPRF_RBF && pl->kind[l] != DGPRF_ARC) return DGPRF_E_ARG;
     if (pl->n_rf[l] < 1 || pl->n_gp[l] < 1 || pl->n_gp[l] > DGPRF_MAX_G) return DGPRF_E_SHAPE;
   }
+  if ((pl->hyp_flags & ~(DGPRF_HYP_KERNEL | DGPRF_HYP_LIK | DGPRF_HYP_MEAN)) != 0 ||
+      (pl->hyp_per_chain != 0 && pl->hyp_per_chain != 1))
+    return DGPRF_E_ARG;
+  for (int l = 0; l < L; ++l)
+    if (pl->ard[l] != 0 && pl->ard[l] != 1) return DGPRF_E_ARG;
   for (int l = L; l < DGPRF_MAX_LAYERS; ++l) {
     pl->kind[l] = 0;
     pl->n_rf[l] = 0;
     pl->n_gp[l] = 0;
+    pl->ard[l] = 0;
   }
   // widths: [d_in, n_gp[:-1]] (+ d_in when input_cat)   models/dgp.py:76-79
   int64_t om = 0, w = 0, lis = 0;
   for (int l = 0; l < DGPRF_MAX_LAYERS; ++l) {
     pl->d[l] = pl->P[l] = pl->ns[l] = pl->cpw[l] = 0;
     pl->omega_off[l] = pl->w_off[l] = pl->lis_off[l] = pl->mean_off[l] = 0;
-    pl->fp_off[l] = pl->dxp_off[l] = 0;
+    pl->fp_off[l] = pl->dxp_off[l] = pl->hpp_off[l] = 0;
   }
   for (int l = 0; l < L; ++l) {
     pl->d[l] = l == 0 ? pl->d_in : pl->n_gp[l - 1] + (pl->input_cat ? pl->d_in : 0);
@@ -202,6 +227,14 @@ int dgprf_plan_init(dgprf_plan_t* pl) {
   ws = align4(ws + (int64_t)pl->n_rt_pad * pl->w_total);
   pl->logp_off = ws;
   ws = align4(ws + B);
+  // full-Bayes partials of each backward workgroup: per input dim sum_b X (dA z^T), sum_b X
+  // rowsum(dA), then sum dPhi * Phi; and the lik_log_var term per row tile
+  for (int l = 0; l < L; ++l) {
+    pl->hpp_off[l] = ws;
+    ws = align4(ws + (int64_t)pl->n_rt_pad * DGPRF_NS_MAX * align4(2 * pl->d[l] + 1));
+  }
+  pl->hpl_off = ws;
+  ws = align4(ws + pl->n_rt_pad);
   pl->yb_cols = pl->likelihood == DGPRF_LIK_SOFTMAX ? 1 : pl->n_gp[L - 1];
   pl->xb_off = ws;
   ws = align4(ws + (int64_t)B * pl->d_in);
@@ -235,9 +268,11 @@ int dgprf_sghmc_step(const dgprf_plan_t* plan, const dgprf_chain_t* chain,
   if (!rc) rc = check_batch(*plan, batch);
   if (!rc) rc = check_step(step);
   if (rc) return rc;
+  if (step->full_bayes && (rc = check_full_bayes(*plan, *chain))) return rc;
   dgprf_step_t st = *step;
   st.grad_only = 0;
-  const StepDev sd = make_step_dev(*plan, *chain, *batch, st.step_offset);
+  StepDev sd = make_step_dev(*plan, *chain, *batch, st.step_offset);
+  sd.full_bayes = st.full_bayes != 0;
   const UpdateDev ud = make_update_dev(st);
   hipError_t e = enqueue_step(*plan, sd, ud, as_stream(stream));
   if (e == hipSuccess) e = dgprf::launch_advance(chain->step, 1, as_stream(stream));
@@ -245,15 +280,17 @@ int dgprf_sghmc_step(const dgprf_plan_t* plan, const dgprf_chain_t* chain,
 }
 
 int dgprf_potential_grad(const dgprf_plan_t* plan, const dgprf_chain_t* chain,
-                         const dgprf_batch_t* batch, float data_size, float* grad_out,
-                         void* stream) {
+                         const dgprf_batch_t* batch, float data_size, int32_t full_bayes,
+                         float* grad_out, void* stream) {
   int rc = check_plan(plan);
   if (!rc) rc = check_chain(chain);
   if (!rc) rc = check_batch(*plan, batch);
   if (rc) return rc;
   if (!grad_out || !(data_size > 0.f)) return DGPRF_E_ARG;
+  if (full_bayes && (rc = check_full_bayes(*plan, *chain))) return rc;
   StepDev sd = make_step_dev(*plan, *chain, *batch, 0);
   sd.grad_out = grad_out;
+  sd.full_bayes = full_bayes != 0;
   dgprf_step_t st;
   std::memset(&st, 0, sizeof(st));
   st.data_size = data_size;
@@ -271,7 +308,10 @@ int dgprf_graph_create_sghmc(dgprf_graph_handle* out, const dgprf_plan_t* plan,
   if (!rc) rc = check_batch(*plan, batch);
   if (!rc) rc = check_step(step);
   if (rc) return rc;
-  if (steps_per_graph < 1 || step->xi || step->xi_resample) return DGPRF_E_ARG;
+  if (steps_per_graph < 1 || step->xi || step->xi_resample || step->xi_hyp ||
+      step->xi_hyp_resample)
+    return DGPRF_E_ARG;
+  if (step->full_bayes && (rc = check_full_bayes(*plan, *chain))) return rc;
   hipStream_t cs;
   if (hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess) return DGPRF_E_HIP;
   hipError_t e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
@@ -279,7 +319,8 @@ int dgprf_graph_create_sghmc(dgprf_graph_handle* out, const dgprf_plan_t* plan,
   st.grad_only = 0;
   const UpdateDev ud = make_update_dev(st);
   for (int k = 0; k < steps_per_graph && e == hipSuccess; ++k) {
-    const StepDev sd = make_step_dev(*plan, *chain, *batch, st.step_offset + k);
+    StepDev sd = make_step_dev(*plan, *chain, *batch, st.step_offset + k);
+    sd.full_bayes = st.full_bayes != 0;
     e = enqueue_step(*plan, sd, ud, cs, k == 0, k + 1 < steps_per_graph);
   }
   if (e == hipSuccess) e = dgprf::launch_advance(chain->step, steps_per_graph, cs);
@@ -438,20 +479,22 @@ int dgprf_sghmc_update(const dgprf_plan_t* plan, float* theta, float* mom, const
 }
 
 int dgprf_welford_update(const dgprf_plan_t* plan, const float* grad, float* mean, float* m2,
-                         int32_t k, void* stream) {
+                         int32_t k, int32_t full_bayes, void* stream) {
   int rc = check_plan(plan);
   if (rc) return rc;
   if (!grad || !mean || !m2 || k < 1) return DGPRF_E_ARG;
-  return hip_rc(dgprf::launch_welford(*plan, grad, mean, m2, k, as_stream(stream)));
+  return hip_rc(dgprf::launch_welford(*plan, grad, mean, m2, k, full_bayes != 0, as_stream(stream)));
 }
 
 int dgprf_mass_estimate(const dgprf_plan_t* plan, const float* mean, const float* m2,
-                        int32_t k_batches, int32_t centered, float* mass_est, void* stream) {
+                        int32_t k_batches, int32_t centered, int32_t full_bayes, float* mass_est,
+                        float* hmass_est, void* stream) {
   int rc = check_plan(plan);
   if (rc) return rc;
   if (!mean || !m2 || !mass_est || k_batches < 1 || (centered && k_batches < 2)) return DGPRF_E_ARG;
-  return hip_rc(
-      dgprf::launch_mass_estimate(*plan, mean, m2, k_batches, centered, mass_est, as_stream(stream)));
+  if (full_bayes && !hmass_est) return DGPRF_E_ARG;
+  return hip_rc(dgprf::launch_mass_estimate(*plan, mean, m2, k_batches, centered, full_bayes != 0,
+                                            mass_est, hmass_est, as_stream(stream)));
 }
 
 }  // extern "C"

@@ -8,15 +8,23 @@
 struct StepDev {
   float* theta;
   float* mom;
-  const float* omega;
-  const float* der;
+  float* omega;
+  float* der;
   const float* mass;
   float* ws;
   const int64_t* step;
-  float* grad_out;  // grad_only mode: [C][w_total]
+  float* grad_out;  // grad_only mode: [C][w_total] (full_bayes: [C][w_total + hyp_total])
   uint64_t seed;
   BatchDev bd;
   int32_t step_offset;
+  int32_t full_bayes;
+  // chain strides of omega / der / hyp (0 = shared by the chains)
+  int64_t om_cs, der_cs, hyp_cs;
+  // full_bayesian=True state
+  const float* z;
+  float* hyp;
+  float* hmom;
+  const float* hmass;
 };
 
 struct UpdateDev {
@@ -25,6 +33,8 @@ struct UpdateDev {
   int64_t start_step, cycle_length;
   const float* xi;
   const float* xi_resample;
+  const float* xi_hyp;
+  const float* xi_hyp_resample;
 };
 
 // In-kernel timestamps for a separate diagnostic build (-DDGPRF_STAMPS); never in the product.
@@ -76,6 +86,9 @@ hipError_t launch_step_fwd(const dgprf_plan_t& pl, const StepDev& sd, int layer,
 hipError_t launch_step_bwd(const dgprf_plan_t& pl, const StepDev& sd, int layer, hipStream_t s);
 hipError_t launch_step_update(const dgprf_plan_t& pl, const StepDev& sd, const UpdateDev& ud,
                               const float* grad_in, hipStream_t s, bool gather_next = false);
+// full_bayesian=True: hyper-parameter gradients / updates and the Omega, c, sigma^2 rebuild
+hipError_t launch_step_hyper(const dgprf_plan_t& pl, const StepDev& sd, const UpdateDev& ud,
+                             hipStream_t s);
 // minibatch rows of step *step + step_offset into the workspace (no-op for DGPRF_BATCH_DIRECT)
 hipError_t launch_gather(const dgprf_plan_t& pl, const StepDev& sd, hipStream_t s);
 hipError_t launch_advance(int64_t* step, int64_t by, hipStream_t s);
@@ -95,13 +108,16 @@ hipError_t launch_prior_w(const dgprf_plan_t& pl, const float* theta, float* out
 
 hipError_t launch_philox_normal(float* out, int64_t n, uint64_t seed, uint64_t sub,
                                 uint32_t purpose, hipStream_t s);
+// Omega / c / sigma^2 of every chain when pl.hyp_per_chain (chain strides omega_total, der_total,
+// hyp_total), else the shared copy.
 hipError_t launch_omega_build(const dgprf_plan_t& pl, const float* z, const float* hyp,
                               float* omega, float* der, hipStream_t s);
 hipError_t launch_rf_omega(int kind, int d, int R, const float* z, const float* lis,
                            const float* mean, const float* log_amp, float* omega, float* c,
                            hipStream_t s);
 hipError_t launch_welford(const dgprf_plan_t& pl, const float* grad, float* mean, float* m2, int k,
-                          hipStream_t s);
+                          bool full_bayes, hipStream_t s);
 hipError_t launch_mass_estimate(const dgprf_plan_t& pl, const float* mean, const float* m2, int K,
-                                int centered, float* mass_est, hipStream_t s);
+                                int centered, bool full_bayes, float* mass_est, float* hmass_est,
+                                hipStream_t s);
 }  // namespace dgprf

@@ -22,6 +22,11 @@ __global__ void k_omega_build(const dgprf_plan_t pl, const float* __restrict__ z
                               const float* __restrict__ hyp, float* __restrict__ omega,
                               float* __restrict__ der) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (pl.hyp_per_chain) {  // chain blockIdx.y: its own hyper-parameters (full_bayesian=True)
+    hyp += (int64_t)blockIdx.y * pl.hyp_total;
+    omega += (int64_t)blockIdx.y * pl.omega_total;
+    der += (int64_t)blockIdx.y * pl.der_total;
+  }
   if (i == 0) {
     for (int l = 0; l < pl.n_layers; ++l) {
       const float amp = expf(hyp[l]);
@@ -70,14 +75,9 @@ __global__ void k_welford(const int64_t total, const float* __restrict__ grad,
   m2[i] = m2[i] + delta * delta2;
 }
 
-// mass_l = sqrt(mean(E[g^2] or Var[g]) + 1e-7) (models/dgp.py:276-288); block per (chain, layer).
-__global__ __launch_bounds__(256) void k_mass(const dgprf_plan_t pl, const float* __restrict__ mean,
-                                              const float* __restrict__ m2, const int K,
-                                              const int centered, float* __restrict__ mass) {
-  __shared__ float red[256];
-  const int layer = blockIdx.x, chain = blockIdx.y;
-  const int64_t cnt = (int64_t)pl.P[layer] * pl.n_gp[layer];
-  const int64_t base = (int64_t)chain * pl.w_total + pl.w_off[layer];
+// sqrt(mean over [base, base + cnt) of E[g^2] (or Var[g]) + 1e-7)  (models/dgp.py:276-288)
+__device__ float mass_of(const float* __restrict__ mean, const float* __restrict__ m2,
+                         int64_t base, int64_t cnt, int K, int centered, float* red) {
   float a = 0.f;
   for (int64_t i = threadIdx.x; i < cnt; i += blockDim.x) {
     const float v = centered ? m2[base + i] / (float)(K - 1)
@@ -90,7 +90,50 @@ __global__ __launch_bounds__(256) void k_mass(const dgprf_plan_t pl, const float
     if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
     __syncthreads();
   }
-  if (threadIdx.x == 0) mass[chain * pl.n_layers + layer] = sqrtf(red[0] / (float)cnt + 1.0e-7f);
+  return sqrtf(red[0] / (float)cnt + 1.0e-7f);
+}
+
+// mass of W_l: block per (chain, layer); cs = chain stride of mean / m2
+__global__ __launch_bounds__(256) void k_mass(const dgprf_plan_t pl, const float* __restrict__ mean,
+                                              const float* __restrict__ m2, const int K,
+                                              const int centered, const int64_t cs,
+                                              float* __restrict__ mass) {
+  __shared__ float red[256];
+  const int layer = blockIdx.x, chain = blockIdx.y;
+  const int64_t cnt = (int64_t)pl.P[layer] * pl.n_gp[layer];
+  const float m = mass_of(mean, m2, (int64_t)chain * cs + pl.w_off[layer], cnt, K, centered, red);
+  if (threadIdx.x == 0) mass[chain * pl.n_layers + layer] = m;
+}
+
+// masses of the trainable hyper-parameter variables (full_bayesian=True), block per
+// (DGPRF_HMASS slot, chain); the hyper gradients follow W in the [w_total + hyp_total] layout.
+__global__ __launch_bounds__(256) void k_hmass(const dgprf_plan_t pl, const float* __restrict__ mean,
+                                               const float* __restrict__ m2, const int K,
+                                               const int centered, float* __restrict__ hmass) {
+  __shared__ float red[256];
+  const int slot = blockIdx.x, chain = blockIdx.y, L = pl.n_layers;
+  const int64_t base = (int64_t)chain * (pl.w_total + pl.hyp_total) + pl.w_total;
+  const bool kern = (pl.hyp_flags & DGPRF_HYP_KERNEL) != 0, mn = (pl.hyp_flags & DGPRF_HYP_MEAN) != 0;
+  const bool lik = (pl.hyp_flags & DGPRF_HYP_LIK) != 0 && pl.likelihood == DGPRF_LIK_GAUSSIAN;
+  int64_t off = -1, cnt = 0;
+  if (slot < 8 && slot < L && kern) {
+    off = slot;  // log_amp
+    cnt = 1;
+  } else if (slot >= 8 && slot < 16 && slot - 8 < L && kern) {
+    const int l = slot - 8;  // log_inv_ls: d_l slots, or one scalar
+    off = pl.lis_off[l];
+    cnt = pl.ard[l] ? pl.d[l] : 1;
+  } else if (slot >= 16 && slot < 24 && slot - 16 < L && mn) {
+    const int l = slot - 16;
+    off = pl.mean_off[l];
+    cnt = pl.d[l];
+  } else if (slot == 24 && lik) {
+    off = L;  // lik_log_var
+    cnt = 1;
+  }
+  float m = 0.f;
+  if (off >= 0) m = mass_of(mean, m2, base + off, cnt, K, centered, red);
+  if (threadIdx.x == 0) hmass[chain * DGPRF_HMASS + slot] = m;
 }
 
 }  // namespace
@@ -109,8 +152,9 @@ hipError_t launch_philox_normal(float* out, int64_t n, uint64_t seed, uint64_t s
 hipError_t launch_omega_build(const dgprf_plan_t& pl, const float* z, const float* hyp,
                               float* omega, float* der, hipStream_t s) {
   const int64_t n = pl.omega_total > 0 ? pl.omega_total : 1;
-  hipLaunchKernelGGL(k_omega_build, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, pl, z, hyp,
-                     omega, der);
+  hipLaunchKernelGGL(k_omega_build,
+                     dim3((unsigned)((n + 255) / 256), pl.hyp_per_chain ? pl.n_chains : 1),
+                     dim3(256), 0, s, pl, z, hyp, omega, der);
   return hipGetLastError();
 }
 
@@ -124,17 +168,22 @@ hipError_t launch_rf_omega(int kind, int d, int R, const float* z, const float* 
 }
 
 hipError_t launch_welford(const dgprf_plan_t& pl, const float* grad, float* mean, float* m2, int k,
-                          hipStream_t s) {
-  const int64_t total = pl.w_total * pl.n_chains;
+                          bool full_bayes, hipStream_t s) {
+  const int64_t total = (pl.w_total + (full_bayes ? pl.hyp_total : 0)) * pl.n_chains;
   hipLaunchKernelGGL(k_welford, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, total, grad,
                      mean, m2, k);
   return hipGetLastError();
 }
 
 hipError_t launch_mass_estimate(const dgprf_plan_t& pl, const float* mean, const float* m2, int K,
-                                int centered, float* mass_est, hipStream_t s) {
+                                int centered, bool full_bayes, float* mass_est, float* hmass_est,
+                                hipStream_t s) {
+  const int64_t cs = pl.w_total + (full_bayes ? pl.hyp_total : 0);
   hipLaunchKernelGGL(k_mass, dim3(pl.n_layers, pl.n_chains), dim3(256), 0, s, pl, mean, m2, K,
-                     centered, mass_est);
+                     centered, cs, mass_est);
+  if (full_bayes)
+    hipLaunchKernelGGL(k_hmass, dim3(DGPRF_HMASS, pl.n_chains), dim3(256), 0, s, pl, mean, m2, K,
+                       centered, hmass_est);
   return hipGetLastError();
 }
 

@@ -167,6 +167,8 @@ __global__ __launch_bounds__(256) void k_forward_rows(
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const FwdLds LD = fwd_lds(pl);
   const int chain = blockIdx.y;
+  const int64_t ochain = pl.hyp_per_chain ? (int64_t)chain * pl.omega_total : 0;
+  const int64_t dchain = pl.hyp_per_chain ? (int64_t)chain * pl.der_total : 0;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, lr = lane & 15, lq = lane >> 4;
   const int64_t row0 = (int64_t)blockIdx.x * TR;
   float* xs = smem;
@@ -189,9 +191,9 @@ __global__ __launch_bounds__(256) void k_forward_rows(
     __syncthreads();
 
     {
-      const float* __restrict__ om = omega + pl.omega_off[layer];
+      const float* __restrict__ om = omega + ochain + pl.omega_off[layer];
       const float* __restrict__ W = Wc + pl.w_off[layer];
-      const float cl = der[layer];
+      const float cl = der[dchain + layer];
       const int NOT = (g + 15) >> 4;
       const bool rbf = pl.kind[layer] == DGPRF_RBF;
       // runtime (layer) -> compile-time body: output tiles, kernel kind, g == 1 VALU path
@@ -237,7 +239,7 @@ __global__ __launch_bounds__(256) void k_forward_rows(
       const float* y = Y + b * y_cols;
       float lp = 0.f, se = 0.f;
       if (pl.likelihood == DGPRF_LIK_GAUSSIAN) {
-        const float var = der[DGPRF_MAX_LAYERS];
+        const float var = der[dchain + DGPRF_MAX_LAYERS];
         const float logvar = logf(var);
         for (int o = 0; o < g; ++o) {
           const float diff = y[o] - f[o];
@@ -628,6 +630,8 @@ void k_forward_tiles(
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const TileLds T = tile_lds(pl, NOTMAX, JO, TPW);
   const int chain = blockIdx.y;
+  const int64_t ochain = pl.hyp_per_chain ? (int64_t)chain * pl.omega_total : 0;
+  const int64_t dchain = pl.hyp_per_chain ? (int64_t)chain * pl.der_total : 0;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, lr = lane & 15, lq = lane >> 4;
   const int64_t wrow0 = (int64_t)blockIdx.x * TW_ROWS * TPW + wave * TR * TPW;
   float* xin = smem + T.xin_off + wave * TPW * TR * T.xin_st;
@@ -643,9 +647,9 @@ void k_forward_tiles(
   for (int e = lane; e < TPW * TR * T.ftst; e += 64) ftw[e] = 0.f;
   __syncthreads();
   for (int layer = 0; layer < L; ++layer) {
-    const float* __restrict__ om = omega + pl.omega_off[layer];
+    const float* __restrict__ om = omega + ochain + pl.omega_off[layer];
     const float* __restrict__ W = Wc + pl.w_off[layer];
-    const float cl = der[layer];
+    const float cl = der[dchain + layer];
     const int g = pl.n_gp[layer], NOT = (g + 15) >> 4;
     const bool rbf = pl.kind[layer] == DGPRF_RBF, ks2 = pl.d[layer] <= 8;
     float* fout = fo.p[layer] ? fo.p[layer] + (int64_t)chain * n * g : nullptr;
@@ -683,7 +687,7 @@ void k_forward_tiles(
       const float* y = Y + b * y_cols;
       float lp = 0.f, se = 0.f;
       if (pl.likelihood == DGPRF_LIK_GAUSSIAN) {
-        const float var = der[DGPRF_MAX_LAYERS];
+        const float var = der[dchain + DGPRF_MAX_LAYERS];
         const float logvar = logf(var);
         for (int o = 0; o < g; ++o) {
           const float diff = y[o] - f[o];

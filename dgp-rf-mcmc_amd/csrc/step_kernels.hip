@@ -40,7 +40,7 @@ __host__ __device__ __forceinline__ int round4(int x) { return (x + 3) & ~3; }
 
 // Arguments of one forward / backward launch of layer `layer` (host-precomputed).
 struct LayerK {
-  const float* om;      // Omega_l [d][R]
+  const float* om;      // Omega_l [d][R] of chain 0 (chain stride om_cs; 0 = shared)
   const float* W;       // W_l [P][g] of chain 0 (chain stride w_cs)
   const float* fprev;   // F_{l-1} partials [NSM][B][gp] of chain 0 (chain stride ws_cs)
   float* fout;          // F_l partials [NSM][B][g]
@@ -52,7 +52,7 @@ struct LayerK {
   const float* yrows;   // minibatch Y rows [B][y_cols] (chain stride yrow_cs)
   const float* cptr;    // c_l
   const float* varptr;  // sigma^2
-  int64_t w_cs, ws_cs, xrow_cs, yrow_cs;
+  int64_t w_cs, ws_cs, xrow_cs, yrow_cs, om_cs, der_cs;
   int32_t d, R, g, gp, dxw, cpw, B, d_in, y_cols;
   int32_t last, likelihood, layer;
   int32_t xst, aux_off, auxst, red_off;
@@ -61,6 +61,11 @@ struct LayerK {
   const float* ws;      // chain 0 workspace (chain stride ws_cs)
   int32_t fast, fprev_off, dsrc_off, xmag, dmag;
   int32_t n_rt, ns, rt_per_xcd;  // XCD-aware block -> (row tile, slice) map
+  // full_bayesian=True (k_step_bwd<..., FB = true>)
+  const float* z;       // z_l [d][R] (shared by the chains)
+  float* hp;            // hyper partials [n_rt_pad][NSM][round4(2d+1)] of chain 0 (stride ws_cs)
+  float* hpl;           // lik_log_var partials [n_rt_pad] (last layer)
+  int32_t hred_off, lik_fb;
 };
 
 // Block -> (row tile, slice): blocks are dealt round-robin over the 8 XCDs, so block b's XCD group
@@ -90,6 +95,7 @@ struct UpdK {
   UpdateDev ud;
   const float* grad_in;
   float* grad_out;
+  int64_t grad_cs;      // chain stride of grad_out (w_total, or w_total + hyp_total in full Bayes)
   // gather of step t+1's minibatch rows (graph mode)
   int32_t gather_next, B, d_in, yb_cols;
   BatchDev bd;
@@ -100,6 +106,21 @@ struct UpdK {
 // v if ok else 0, written so that the compiler cannot sink the (always in-range, finite) load
 // into an exec-masked branch followed by an immediate wait: the load result is used on every path.
 __device__ __forceinline__ float keep(float v, bool ok) { return v * (ok ? 1.f : 0.f); }
+
+// Sum over each 16-lane row of the wave (ds_swizzle xor butterflies, fixed order; every lane of
+// the row ends with the same value).
+template <int XM>
+__device__ __forceinline__ float swz_xor(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v),
+                                                               (XM << 10) | 0x1F));
+}
+__device__ __forceinline__ float sum16(float v) {
+  v += swz_xor<8>(v);
+  v += swz_xor<4>(v);
+  v += swz_xor<2>(v);
+  v += swz_xor<1>(v);
+  return v;
+}
 
 // sum over the DGPRF_NS_MAX slices of a partial buffer: independent loads, fixed order.
 __device__ __forceinline__ float sum_slices(const float* __restrict__ p, int64_t stride) {
@@ -301,6 +322,7 @@ __global__ __launch_bounds__(256) void k_step_fwd(const LayerK a) {
   int rt, sl;
   if (!tile_of_block(a, rt, sl)) return;
   const int chain = blockIdx.z;
+  const float* __restrict__ om = a.om + (int64_t)chain * a.om_cs;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, lr = lane & 15, lq = lane >> 4;
   const int R = a.R, g = a.g, d = a.d, B = a.B, cpw = a.cpw;
   const int row0 = rt * TR;
@@ -313,9 +335,9 @@ __global__ __launch_bounds__(256) void k_step_fwd(const LayerK a) {
 
   // first chunk's fragments: independent of the X tile, issued first
   float omk[8], wf[NOT][4][2];
-  if (KS > 0) load_om_frag<KS>(a.om, R, d, chunk_f0(0), lr, lq, omk);
+  if (KS > 0) load_om_frag<KS>(om, R, d, chunk_f0(0), lr, lq, omk);
   load_w_frag<NOT, RBF, G1>(W, R, g, chunk_f0(0), lr, lq, wf);
-  const float cl = *a.cptr;
+  const float cl = a.cptr[(int64_t)chain * a.der_cs];
   DGPRF_STAMP(stamp_base, 1);
   if (a.fast) {
     elem_prologue(a, chain, row0, 0, xs, red, 0, red, red);  // no dF tile: unused targets
@@ -337,7 +359,7 @@ __global__ __launch_bounds__(256) void k_step_fwd(const LayerK a) {
   for (int i = 0; i < cpw; ++i) {
     const int f0 = chunk_f0(i);
     if (f0 >= R) break;
-    const f4 at = a_tile<KS, false>(a.om, R, d, f0, omk, xf, xs, a.xst, lr, lq);
+    const f4 at = a_tile<KS, false>(om, R, d, f0, omk, xf, xs, a.xst, lr, lq);
     float p0[4], p1[4];
     features<RBF>(at, cl, p0, p1);
     float wc[NOT][4][2];
@@ -350,7 +372,7 @@ __global__ __launch_bounds__(256) void k_step_fwd(const LayerK a) {
         wc[ot][r][1] = keep(wf[ot][r][1], ok);
       }
     if (i + 1 < cpw) {  // prefetch the next chunk (clamped loads are always in range)
-      if (KS > 0) load_om_frag<KS>(a.om, R, d, chunk_f0(i + 1), lr, lq, omk);
+      if (KS > 0) load_om_frag<KS>(om, R, d, chunk_f0(i + 1), lr, lq, omk);
       load_w_frag<NOT, RBF, G1>(W, R, g, chunk_f0(i + 1), lr, lq, wf);
     }
     if (G1) {
@@ -403,12 +425,13 @@ __global__ __launch_bounds__(256) void k_step_fwd(const LayerK a) {
 }
 
 // ------------------------------------------------------------------------- backward
-template <int KS, int NOT, bool RBF, bool G1>
+template <int KS, int NOT, bool RBF, bool G1, bool FB>
 __global__ __launch_bounds__(256) void k_step_bwd(const LayerK a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   int rt, sl;
   if (!tile_of_block(a, rt, sl)) return;
   const int chain = blockIdx.z;
+  const float* __restrict__ om = a.om + (int64_t)chain * a.om_cs;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, lr = lane & 15, lq = lane >> 4;
   const int R = a.R, g = a.g, d = a.d, B = a.B, cpw = a.cpw, dxw = a.dxw;
   const int row0 = rt * TR;
@@ -422,10 +445,12 @@ __global__ __launch_bounds__(256) void k_step_bwd(const LayerK a) {
   auto chunk_f0 = [&](int i) { return ((sl * cpw + i) * NW + wave) * 16; };
   constexpr int KGM = 4 * NOT;  // k-steps of the dPhi contraction (K = g)
   const int ND = (dxw + 15) >> 4;
+  // dPhi / dA are needed for dX (l > 0) and, with full_bayesian=True, for every layer
+  const bool dphi = FB || dxw > 0;
 
   // first chunk's fragments, issued before the dependent partial sums
   float omk[8];
-  if (KS > 0) load_om_frag<KS>(a.om, R, d, chunk_f0(0), lr, lq, omk);
+  if (KS > 0) load_om_frag<KS>(om, R, d, chunk_f0(0), lr, lq, omk);
   // dPhi / dX A operands (W_l rows and Omega_l rows of this workgroup's 64-feature block) are
   // staged through LDS as W [2][64*g] (raw rows) and Omega [rows][OST]; the fragment reads zero
   // feature rows >= R.
@@ -446,8 +471,8 @@ __global__ __launch_bounds__(256) void k_step_bwd(const LayerK a) {
     }
 #pragma unroll
     for (int j = 0; j < NJO; ++j) {
-      const int e = min((int)threadIdx.x + 256 * j, nom - 1);
-      sto[j] = a.om[(int64_t)(e >> 6) * R + min(fb + (e & 63), R - 1)];
+      const int e = min((int)threadIdx.x + 256 * j, max(nom - 1, 0));
+      sto[j] = om[(int64_t)(e >> 6) * R + min(fb + (e & 63), R - 1)];
     }
   };
   auto stage_store = [&](int fb) {
@@ -463,7 +488,7 @@ __global__ __launch_bounds__(256) void k_step_bwd(const LayerK a) {
     }
   };
   const int fb0 = (sl * cpw) * 64;
-  const float cl = *a.cptr;
+  const float cl = a.cptr[(int64_t)chain * a.der_cs];
   const float* fpl = a.fout + (int64_t)chain * a.ws_cs;        // F_L partials (last layer)
   const float* dxn = a.dxnext + (int64_t)chain * a.ws_cs;      // dX_{l+1} partials
   const float* yr = a.yrows + (int64_t)chain * a.yrow_cs;
@@ -472,7 +497,7 @@ __global__ __launch_bounds__(256) void k_step_bwd(const LayerK a) {
   if (a.fast) {
     // ---- single burst: W/Omega block, X tile, dF (or F_L) partials and Y rows
     f4 sw[2], so;
-    if (dxw > 0) {
+    if (dphi) {
       const rsrc_t rw = make_rsrc(W, (int64_t)(RBF ? 2 : 1) * R * g);
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
@@ -480,20 +505,20 @@ __global__ __launch_bounds__(256) void k_step_bwd(const LayerK a) {
         const uint32_t off = (uint32_t)((((h * R) + fb0) * g + 4 * q) * 4);
         sw[j] = bload4(rw, i < (RBF ? 32 : 16) * g ? off : DGPRF_OOB);
       }
-      const rsrc_t ro = make_rsrc(a.om, (int64_t)dxw * R);
+      const rsrc_t ro = make_rsrc(om, (int64_t)dxw * R);
       const int k = threadIdx.x >> 4, c4 = threadIdx.x & 15;
       so = bload4(ro, k < dxw && fb0 + 4 * c4 < R ? (uint32_t)((k * R + fb0 + 4 * c4) * 4) : DGPRF_OOB);
     }
     DGPRF_STAMP(stamp_base, 1);
     elem_prologue(a, chain, row0, TR * g, xs, dfs, dfst, ysh, red);
-    if (dxw > 0) {
+    if (dphi) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) *reinterpret_cast<f4*>(wsl + 4 * ((int)threadIdx.x + 256 * j)) = sw[j];
       *reinterpret_cast<f4*>(osl + (threadIdx.x >> 4) * OST + 4 * (threadIdx.x & 15)) = so;
     }
     DGPRF_STAMP(stamp_base, 4);
   } else {
-    if (dxw > 0) stage_load(fb0);
+    if (dphi) stage_load(fb0);
     load_x_tile(a, chain, row0, xs);
     for (int e = threadIdx.x; e < TR * g; e += blockDim.x) {  // dF (or F_L) slice sums; Y alongside
       const int r = e / g, o = e - r * g, b = row0 + r, bc = min(b, B - 1);
@@ -511,18 +536,22 @@ __global__ __launch_bounds__(256) void k_step_bwd(const LayerK a) {
     if (threadIdx.x < TR) {
       const int r = threadIdx.x, b = row0 + r;
       float* df = dfs + r * dfst;
+      float lvrow = 0.f;
       if (b < B) {
         const float* y = ysh + r * dfst;
         const float invB = 1.0f / (float)B;
         float logp = 0.f;
         if (a.likelihood == DGPRF_LIK_GAUSSIAN) {
-          const float var = *a.varptr;
+          const float var = a.varptr[(int64_t)chain * a.der_cs];
           const float logvar = logf(var);
+          float lv = 0.f;  // d(-log p)/d lik_log_var = sum_o (1 - diff^2/var)/2
           for (int o = 0; o < g; ++o) {
             const float diff = y[o] - df[o];
             logp += -0.5f * (LOG_2PI + logvar + diff * diff / var);
             df[o] = -(diff / var) * invB;
+            lv += 0.5f * (1.f - diff * diff / var);
           }
+          lvrow = lv * invB;
         } else {
           float mx = -INFINITY;
           for (int o = 0; o < g; ++o) mx = fmaxf(mx, df[o]);
@@ -538,9 +567,13 @@ __global__ __launch_bounds__(256) void k_step_bwd(const LayerK a) {
         }
         if (sl == 0) a.logp[(int64_t)chain * a.ws_cs + b] = logp;
       }
+      if (FB && a.lik_fb) {  // the row tile's lik_log_var partial (lanes 0..15, fixed order)
+        const float v = sum16(lvrow);
+        if (r == 0 && sl == 0) a.hpl[(int64_t)chain * a.ws_cs + rt] = v;
+      }
     }
   }
-  if (!a.fast && dxw > 0) stage_store(fb0);
+  if (!a.fast && dphi) stage_store(fb0);
   __syncthreads();
   DGPRF_STAMP(stamp_base, 2);
 
@@ -572,12 +605,21 @@ __global__ __launch_bounds__(256) void k_step_bwd(const LayerK a) {
 
   float* gwp = a.gwp + (int64_t)chain * a.ws_cs + (int64_t)rt * a.w_cs;
   f4 dxa[4] = {f4zero(), f4zero(), f4zero(), f4zero()};
+  // full_bayesian=True: per-wave sums over this row tile and the wave's features of
+  //   hw[k]     = sum_b X[b][k] (dA z^T)[b][k]   (-> log_inv_ls)
+  //   hw[d + k] = sum_b X[b][k] rowsum(dA)[b]    (-> mean)
+  //   hw[2d]    = sum dPhi * Phi                  (-> log_amp)
+  const int hst = round4(2 * d + 1);
+  float* hw = smem + a.hred_off + wave * hst;
+  float ampl = 0.f;
+  if (FB)
+    for (int e = lane; e < hst; e += 64) hw[e] = 0.f;
   for (int i = 0; i < cpw; ++i) {
     const int f0 = chunk_f0(i);
     if (f0 >= R) break;
     if (i > 0) {
-      if (KS > 0) load_om_frag<KS>(a.om, R, d, f0, lr, lq, omk);
-      if (dxw > 0) {
+      if (KS > 0) load_om_frag<KS>(om, R, d, f0, lr, lq, omk);
+      if (dphi) {
         stage_load((sl * cpw + i) * 64);
         __syncthreads();  // every wave is done with the previous block
         stage_store((sl * cpw + i) * 64);
@@ -590,7 +632,7 @@ __global__ __launch_bounds__(256) void k_step_bwd(const LayerK a) {
     //   dPhi = dF W^T in the features-in-registers orientation (K = g)
     float wd0[KGM], wd1[KGM];
     f4 oxv[4];
-    if (dxw > 0) {
+    if (dphi) {
       const bool frow = f0 + lr < R;
 #pragma unroll
       for (int ks = 0; ks < KGM; ++ks) {
@@ -604,10 +646,10 @@ __global__ __launch_bounds__(256) void k_step_bwd(const LayerK a) {
       for (int dt = 0; dt < 4; ++dt)
         oxv[dt] = *reinterpret_cast<const f4*>(osl + (dt * 16 + lr) * OST + wave * 16 + 4 * lq);
     }
-    const f4 at_t = a_tile<KS, true>(a.om, R, d, f0, omk, xf, xs, a.xst, lr, lq);
+    const f4 at_t = a_tile<KS, true>(om, R, d, f0, omk, xf, xs, a.xst, lr, lq);
     f4 at_n = f4zero(), dpc = f4zero(), dps = f4zero();
-    if (dxw > 0) {
-      at_n = a_tile<KS, false>(a.om, R, d, f0, omk, xf, xs, a.xst, lr, lq);
+    if (dphi) {
+      at_n = a_tile<KS, false>(om, R, d, f0, omk, xf, xs, a.xst, lr, lq);
       if (G1) {
         // g == 1: dPhi[b][f] = dF[b] W[f] (outer product, VALU)
 #pragma unroll
@@ -631,15 +673,17 @@ __global__ __launch_bounds__(256) void k_step_bwd(const LayerK a) {
     float q0[4], q1[4];
     features<RBF>(at_t, cl, q0, q1);
     float da[4];
-    if (dxw > 0) {
+    if (dphi) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         if (RBF) {
           float sv, cv;
           rf_sincos(at_n[r], &sv, &cv);
           da[r] = -(cl * sv) * dpc[r] + (cl * cv) * dps[r];
+          if (FB) ampl += dpc[r] * (cl * cv) + dps[r] * (cl * sv);
         } else {
           da[r] = at_n[r] > 0.f ? cl * dpc[r] : 0.f;
+          if (FB) ampl += dpc[r] * (cl * fmaxf(at_n[r], 0.f));
         }
       }
     }
@@ -697,8 +741,49 @@ __global__ __launch_bounds__(256) void k_step_bwd(const LayerK a) {
           for (int r = 0; r < 4; ++r) dxa[dt] = mfma16(oxv[dt][r], da[r], dxa[dt]);
         }
     }
+    if (FB) {
+      // rowsum(dA) over this chunk: the lane's 4 features, then the 4 feature groups
+      float rs = (da[0] + da[1]) + (da[2] + da[3]);
+      rs += __shfl_xor(rs, 16);
+      rs += __shfl_xor(rs, 32);
+      // Dz = dA z^T in 16-dim tiles of the layer input (same contraction as dX with z rows),
+      // contracted with the X tile over the 16 rows right away (linear in the features)
+      const rsrc_t rz = make_rsrc(a.z, (int64_t)d * R);
+      for (int dt = 0; dt * 16 < d; ++dt) {
+        const int k = dt * 16 + lr;
+        const f4 zf = bload4(rz, k < d && f0 + 4 * lq < R
+                                     ? (uint32_t)(((int64_t)k * R + f0 + 4 * lq) * 4) : DGPRF_OOB);
+        f4 dz = f4zero();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dz = mfma16(zf[r], da[r], dz);
+        // dz[r] = Dz[row lr][dt*16 + 4lq + r]
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int kk = dt * 16 + 4 * lq + r;
+          const float xv = kk < d ? xs[lr * a.xst + kk] : 0.f;
+          const float s1 = sum16(xv * dz[r]);
+          const float s2 = sum16(xv * rs);
+          if (lr == 0 && kk < d) {
+            hw[kk] += s1;
+            hw[d + kk] += s2;
+          }
+        }
+      }
+    }
   }
   DGPRF_STAMP(stamp_base, 3);
+  if (FB) {
+    // log_amp term over the wave, then the workgroup's partial row [2d+1] in wave order
+    float v = sum16(ampl);
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    if (lane == 0) hw[2 * d] = v;
+    __syncthreads();
+    float* hp = a.hp + (int64_t)chain * a.ws_cs + ((int64_t)rt * NSM + sl) * hst;
+    const float* h0 = smem + a.hred_off;
+    for (int e = threadIdx.x; e < 2 * d + 1; e += blockDim.x)
+      hp[e] = ((h0[e] + h0[hst + e]) + h0[2 * hst + e]) + h0[3 * hst + e];
+  }
   if (dxw > 0) {
     // dxa[dt][r] = dX[row lr][dt*16 + 4lq + r]; sum the 4 waves in LDS, store the slice partial.
     const int DP = ND * 16;
@@ -840,7 +925,7 @@ __global__ __launch_bounds__(UPD_THREADS) void k_step_update(const UpdK a) {
   // dU/dW = W/N (prior N(0,1), models/dgp.py:129-136,171) + Phi^T dF (likelihood)
   if (!GIN) gr = th / N + gr;
   if (GONLY) {
-    if (live) st2(a.grad_out + cw + e0, gr);
+    if (live) st2(a.grad_out + (int64_t)chain * a.grad_cs + e0, gr);
     return;
   }
   const float M = a.mass[chain * a.n_layers + layer];
@@ -894,6 +979,191 @@ __global__ __launch_bounds__(UPD_THREADS) void k_step_update(const UpdK a) {
   DGPRF_STAMP(stamp_base, 14);
 }
 
+// ------------------------------------------------------------------------- hyper-parameters
+// full_bayesian=True (models/dgp.py:175-181, 199-216): one workgroup per layer (+ one for the
+// Gaussian lik_log_var) reduces the backward's per-workgroup partials in a fixed order, forms
+//   g_log_amp   = sum dPhi*Phi                          + log_amp/N
+//   g_lis[k]    = exp(lis[k]) sum_b X[b][k](dA z^T)[b][k] + lis[k]/N   (scalar lis: summed over k)
+//   g_mean[k]   = sum_b X[b][k] rowsum(dA)[b]           + mean[k]/N
+//   g_lik       = sum_b sum_o (1 - (y-F)^2/var)/(2B)    + lik_log_var/N
+// applies the same SGHMC update as W (own momentum, mass and Philox stream) and rebuilds the
+// layer's Omega / c (and sigma^2), so the next step sees the new hyper-parameters.
+struct HypK {
+  float* hyp;  // chain 0 (chain stride hyp_cs)
+  float* hmom;  // [C][hyp_total]
+  const float* hmass;
+  const float* z;
+  float* omega;
+  float* der;
+  const float* ws;
+  const int64_t* step;
+  float* grad_out;
+  uint64_t seed;
+  int64_t ws_cs, hyp_cs, om_cs, der_cs, hyp_total, grad_cs, w_total;
+  int32_t n_layers, n_rt, step_offset, flags, likelihood, vt;
+  int32_t d[DGPRF_MAX_LAYERS], R[DGPRF_MAX_LAYERS], kind[DGPRF_MAX_LAYERS], ard[DGPRF_MAX_LAYERS];
+  int32_t ns[DGPRF_MAX_LAYERS];
+  int64_t lis_off[DGPRF_MAX_LAYERS], mean_off[DGPRF_MAX_LAYERS], om_off[DGPRF_MAX_LAYERS];
+  int64_t hpp_off[DGPRF_MAX_LAYERS], hpl_off;
+  UpdateDev ud;
+};
+
+__device__ __forceinline__ float normal_at(uint64_t seed, uint64_t t, uint32_t purpose,
+                                           uint32_t chain, int64_t slot) {
+  const f4 z = philox_normal4(seed, t, purpose, chain, (uint32_t)(slot >> 2));
+  return z[slot & 3];
+}
+
+template <bool GONLY, bool XI, bool CYC>
+__global__ __launch_bounds__(256) void k_step_hyper(const HypK a) {
+  extern __shared__ __attribute__((aligned(16))) float hsm[];
+  const int chain = blockIdx.y, blk = blockIdx.x, L = a.n_layers, tid = threadIdx.x;
+  float* hyp = a.hyp + (int64_t)chain * a.hyp_cs;
+  float* hm = a.hmom + (int64_t)chain * a.hyp_total;
+  const UpdateDev& ud = a.ud;
+  const float N = ud.data_size;
+  const int64_t t = *a.step + (int64_t)a.step_offset;
+  float lr = ud.lr, T = ud.temperature;
+  int resample = ud.resample;
+  if (CYC) {
+    if (t < ud.start_step) {
+      T = 0.f;
+      resample = 0;
+    } else {
+      const int64_t si = t - ud.start_step + 1;
+      const float rate = cyclical_rate(si, ud.cycle_length);
+      lr = ud.lr * (rate * rate);
+      T = 1.f;
+      resample = ud.resample_head && (si % ud.cycle_length == 1);
+    }
+  }
+  const float h = sqrtf(lr / N), beta = ud.beta;
+  // SGHMC update of hyper slot `slot` with gradient g (models/dgp.py:206-216); returns the value
+  auto upd = [&](int64_t slot, float g, int midx, float* mom_out) -> float {
+    if (GONLY) {
+      a.grad_out[(int64_t)chain * a.grad_cs + a.w_total + slot] = g;
+      return hyp[slot];
+    }
+    const float M = a.hmass[chain * DGPRF_HMASS + midx];
+    float m = hm[slot];
+    if (resample)
+      m = (XI && ud.xi_hyp_resample)
+              ? ud.xi_hyp_resample[(int64_t)chain * a.hyp_total + slot]
+              : normal_at(a.seed, (uint64_t)t, DGPRF_RNG_HYPER_RESAMPLE, chain, slot);
+    const float eps = (XI && ud.xi_hyp) ? ud.xi_hyp[(int64_t)chain * a.hyp_total + slot]
+                                        : normal_at(a.seed, (uint64_t)t, DGPRF_RNG_HYPER, chain, slot);
+    const float mn = beta * m - (h * N) * g + sqrtf(2.0f * (1.0f - beta) * T * M) * eps;
+    *mom_out = mn;
+    return hyp[slot] + (h * (1.0f / M)) * mn;
+  };
+  if (blk == L) {  // Gaussian lik_log_var
+    if ((a.flags & DGPRF_HYP_LIK) && a.likelihood == DGPRF_LIK_GAUSSIAN && tid == 0) {
+      const float* hpl = a.ws + (int64_t)chain * a.ws_cs + a.hpl_off;
+      float s = 0.f;
+      for (int rt = 0; rt < a.n_rt; ++rt) s += hpl[rt];
+      float mn = 0.f;
+      const float v = upd(L, s + hyp[L] / N, 24, &mn);
+      if (!GONLY) {
+        hm[L] = mn;
+        hyp[L] = v;
+        a.der[(int64_t)chain * a.der_cs + DGPRF_MAX_LAYERS] = expf(v);
+      }
+    }
+    return;
+  }
+  const int l = blk, d = a.d[l], R = a.R[l], nv = 2 * d + 1, hs = (nv + 3) & ~3;
+  const int ns = a.ns[l], P = a.n_rt * ns, vt = a.vt;
+  float* stage = hsm;                   // [P][vt]
+  float* tot = hsm + P * vt;            // [hs]
+  float* red = tot + hs;                // [256]
+  const float* hp = a.ws + (int64_t)chain * a.ws_cs + a.hpp_off[l];
+  const rsrc_t rh = make_rsrc(hp, (int64_t)a.n_rt * NSM * hs);
+  // fixed-order sums over (row tile, slice) of every value, vt values at a time through LDS
+  for (int e0 = 0; e0 < nv; e0 += vt) {
+    const int q4 = vt >> 2;
+    for (int i = tid; i < P * q4; i += 256) {
+      const int row = i / q4, q = i - row * q4, rt = row / ns, sl = row - rt * ns;
+      const int e = e0 + 4 * q;
+      const f4 v = bload4(rh, e < hs ? (uint32_t)((((int64_t)rt * NSM + sl) * hs + e) * 4) : DGPRF_OOB);
+      *reinterpret_cast<f4*>(stage + row * vt + 4 * q) = v;
+    }
+    __syncthreads();
+    for (int e = tid; e < vt && e0 + e < nv; e += 256) {
+      float acc = 0.f;
+      for (int row = 0; row < P; ++row) acc += stage[row * vt + e];
+      tot[e0 + e] = acc;
+    }
+    __syncthreads();
+  }
+  const int64_t lis = a.lis_off[l], mo = a.mean_off[l];
+  if (a.flags & DGPRF_HYP_KERNEL) {
+    if (tid == 0) {
+      float mn = 0.f;
+      const float v = upd(l, tot[2 * d] + hyp[l] / N, l, &mn);
+      if (!GONLY) {
+        hm[l] = mn;
+        hyp[l] = v;
+      }
+    }
+    if (a.ard[l]) {
+      for (int k = tid; k < d; k += 256) {
+        const float lk = hyp[lis + k];
+        float mn = 0.f;
+        const float v = upd(lis + k, expf(lk) * tot[k] + lk / N, 8 + l, &mn);
+        if (!GONLY) {
+          hm[lis + k] = mn;
+          hyp[lis + k] = v;
+        }
+      }
+    } else {  // one scalar length scale: its gradient sums over the d dims
+      float part = 0.f;
+      for (int k = tid; k < d; k += 256) part += expf(hyp[lis + k]) * tot[k];
+      red[tid] = part;
+      __syncthreads();
+      for (int w = 128; w > 0; w >>= 1) {
+        if (tid < w) red[tid] += red[tid + w];
+        __syncthreads();
+      }
+      if (tid == 0) {
+        float mn = 0.f;
+        const float v = upd(lis, red[0] + hyp[lis] / N, 8 + l, &mn);
+        if (GONLY) {
+          for (int k = 1; k < d; ++k) a.grad_out[(int64_t)chain * a.grad_cs + a.w_total + lis + k] =
+              a.grad_out[(int64_t)chain * a.grad_cs + a.w_total + lis];
+        } else {
+          for (int k = 0; k < d; ++k) {
+            hm[lis + k] = mn;
+            hyp[lis + k] = v;
+          }
+        }
+      }
+    }
+  }
+  if (a.flags & DGPRF_HYP_MEAN) {
+    for (int k = tid; k < d; k += 256) {
+      float mn = 0.f;
+      const float v = upd(mo + k, tot[d + k] + hyp[mo + k] / N, 16 + l, &mn);
+      if (!GONLY) {
+        hm[mo + k] = mn;
+        hyp[mo + k] = v;
+      }
+    }
+  }
+  if (GONLY) return;
+  __syncthreads();  // this layer's new hyper-parameters are in place
+  // Omega_l = exp(lis)[:,None] z_l + mean[:,None], c_l (kernels/RBF.py:43-53, rf_layers.py:34-44)
+  float* om = a.omega + (int64_t)chain * a.om_cs + a.om_off[l];
+  const float* zl = a.z + a.om_off[l];
+  for (int64_t i = tid; i < (int64_t)d * R; i += 256) {
+    const int k = (int)(i / R);
+    om[i] = expf(hyp[lis + k]) * zl[i] + hyp[mo + k];
+  }
+  if (tid == 0) {
+    const float amp = expf(hyp[l]), sq = sqrtf((float)R);
+    a.der[(int64_t)chain * a.der_cs + l] = a.kind[l] == DGPRF_RBF ? amp / sq : (sqrtf(2.f) * amp) / sq;
+  }
+}
+
 __global__ void k_advance(int64_t* step, int64_t by) {
   if (threadIdx.x == 0 && blockIdx.x == 0) *step += by;
 }
@@ -917,6 +1187,8 @@ LayerK make_layer_k(const dgprf_plan_t& pl, const StepDev& sd, int l, int& lds_f
   a.y_cols = direct ? sd.bd.y_cols : pl.yb_cols;
   a.cptr = sd.der + l;
   a.varptr = sd.der + DGPRF_MAX_LAYERS;
+  a.om_cs = sd.om_cs;
+  a.der_cs = sd.der_cs;
   a.w_cs = pl.w_total;
   a.ws_cs = pl.ws_chain;
   a.d = pl.d[l];
@@ -943,6 +1215,13 @@ LayerK make_layer_k(const dgprf_plan_t& pl, const StepDev& sd, int l, int& lds_f
   a.n_rt = pl.n_row_tiles;
   a.ns = pl.ns[l];
   a.rt_per_xcd = (pl.n_row_tiles + 7) / 8;
+  // full_bayesian=True: z rows, hyper partials, per-wave LDS sums [4][round4(2d+1)]
+  a.z = sd.z ? sd.z + pl.omega_off[l] : nullptr;
+  a.hp = sd.ws + pl.hpp_off[l];
+  a.hpl = sd.ws + pl.hpl_off;
+  a.lik_fb = (pl.hyp_flags & DGPRF_HYP_LIK) != 0 && pl.likelihood == DGPRF_LIK_GAUSSIAN;
+  a.hred_off = lds_floats;
+  if (sd.full_bayes) lds_floats += NW * round4(2 * a.d + 1);
   return a;
 }
 
@@ -979,7 +1258,42 @@ LayerK make_layer_k(const dgprf_plan_t& pl, const StepDev& sd, int l, int& lds_f
   }
 
 DGPRF_KS_NOT_DISPATCH(k_step_fwd)
-DGPRF_KS_NOT_DISPATCH(k_step_bwd)
+
+// backward: KS x NOT x RBF x G1 x FB
+template <int KS, int NOT, bool G1>
+void k_step_bwd_launch3(bool rbf, bool fb, dim3 grid, size_t lds, hipStream_t s, const LayerK& a) {
+#define DGPRF_BWD(R_, F_)                                                             \
+  do {                                                                               \
+    dgprf::set_lds_limit((const void*)k_step_bwd<KS, NOT, R_, G1, F_>, lds);        \
+    hipLaunchKernelGGL((k_step_bwd<KS, NOT, R_, G1, F_>), grid, dim3(256), lds, s, a); \
+  } while (0)
+  if (rbf) {
+    if (fb) DGPRF_BWD(true, true);
+    else DGPRF_BWD(true, false);
+  } else {
+    if (fb) DGPRF_BWD(false, true);
+    else DGPRF_BWD(false, false);
+  }
+#undef DGPRF_BWD
+}
+template <int KS>
+void k_step_bwd_launch2(int g, bool rbf, bool fb, dim3 grid, size_t lds, hipStream_t s,
+                        const LayerK& a) {
+  const int NOT = (g + 15) >> 4;
+  if (g == 1) k_step_bwd_launch3<KS, 1, true>(rbf, fb, grid, lds, s, a);
+  else if (NOT == 1) k_step_bwd_launch3<KS, 1, false>(rbf, fb, grid, lds, s, a);
+  else if (NOT == 2) k_step_bwd_launch3<KS, 2, false>(rbf, fb, grid, lds, s, a);
+  else if (NOT == 3) k_step_bwd_launch3<KS, 3, false>(rbf, fb, grid, lds, s, a);
+  else k_step_bwd_launch3<KS, 4, false>(rbf, fb, grid, lds, s, a);
+}
+void k_step_bwd_launch(int d, int g, bool rbf, bool fb, dim3 grid, size_t lds, hipStream_t s,
+                       const LayerK& a) {
+  if (d <= 4) k_step_bwd_launch2<1>(g, rbf, fb, grid, lds, s, a);
+  else if (d <= 8) k_step_bwd_launch2<2>(g, rbf, fb, grid, lds, s, a);
+  else if (d <= 16) k_step_bwd_launch2<4>(g, rbf, fb, grid, lds, s, a);
+  else if (d <= 32) k_step_bwd_launch2<8>(g, rbf, fb, grid, lds, s, a);
+  else k_step_bwd_launch2<0>(g, rbf, fb, grid, lds, s, a);
+}
 
 }  // namespace
 
@@ -1011,7 +1325,8 @@ hipError_t launch_step_bwd(const dgprf_plan_t& pl, const StepDev& sd, int layer,
   int lds_floats = 0;
   const LayerK a = make_layer_k(pl, sd, layer, lds_floats);
   dim3 grid(8 * a.rt_per_xcd * a.ns, 1, pl.n_chains);
-  k_step_bwd_launch(pl.d[layer], pl.n_gp[layer], pl.kind[layer] == DGPRF_RBF, grid,
+  k_step_bwd_launch(pl.d[layer], pl.n_gp[layer], pl.kind[layer] == DGPRF_RBF, sd.full_bayes != 0,
+                    grid,
                     (size_t)lds_floats * sizeof(float), s, a);
   return hipGetLastError();
 }
@@ -1040,6 +1355,7 @@ hipError_t launch_step_update(const dgprf_plan_t& pl, const StepDev& sd, const U
   a.ud = ud;
   a.grad_in = grad_in;
   a.grad_out = sd.grad_out;
+  a.grad_cs = pl.w_total + (sd.full_bayes ? pl.hyp_total : 0);
   a.gather_next = gather_next && sd.bd.mode == DGPRF_BATCH_EPOCH ? 1 : 0;
   a.B = pl.batch;
   a.d_in = pl.d_in;
@@ -1068,6 +1384,76 @@ hipError_t launch_step_update(const dgprf_plan_t& pl, const StepDev& sd, const U
     DGPRF_UPD_CASE(12) DGPRF_UPD_CASE(13) DGPRF_UPD_CASE(14) DGPRF_UPD_CASE(15)
   }
 #undef DGPRF_UPD_CASE
+  return hipGetLastError();
+}
+
+hipError_t launch_step_hyper(const dgprf_plan_t& pl, const StepDev& sd, const UpdateDev& ud,
+                             hipStream_t s) {
+  HypK a;
+  a.hyp = sd.hyp;
+  a.hmom = sd.hmom;
+  a.hmass = sd.hmass;
+  a.z = sd.z;
+  a.omega = sd.omega;
+  a.der = sd.der;
+  a.ws = sd.ws;
+  a.step = sd.step;
+  a.grad_out = sd.grad_out;
+  a.seed = sd.seed;
+  a.ws_cs = pl.ws_chain;
+  a.hyp_cs = sd.hyp_cs;
+  a.om_cs = sd.om_cs;
+  a.der_cs = sd.der_cs;
+  a.hyp_total = pl.hyp_total;
+  a.grad_cs = pl.w_total + pl.hyp_total;
+  a.w_total = pl.w_total;
+  a.n_layers = pl.n_layers;
+  a.n_rt = pl.n_row_tiles;
+  a.step_offset = sd.step_offset;
+  a.flags = pl.hyp_flags;
+  a.likelihood = pl.likelihood;
+  int hsmax = 4, pmax = 1;
+  for (int l = 0; l < DGPRF_MAX_LAYERS; ++l) {
+    const bool on = l < pl.n_layers;
+    a.d[l] = on ? pl.d[l] : 0;
+    a.R[l] = on ? pl.n_rf[l] : 0;
+    a.kind[l] = on ? pl.kind[l] : 0;
+    a.ard[l] = on ? pl.ard[l] : 0;
+    a.ns[l] = on ? pl.ns[l] : 0;
+    a.lis_off[l] = on ? pl.lis_off[l] : 0;
+    a.mean_off[l] = on ? pl.mean_off[l] : 0;
+    a.om_off[l] = on ? pl.omega_off[l] : 0;
+    a.hpp_off[l] = on ? pl.hpp_off[l] : 0;
+    if (on) {
+      hsmax = max(hsmax, round4(2 * pl.d[l] + 1));
+      pmax = max(pmax, pl.n_row_tiles * pl.ns[l]);
+    }
+  }
+  a.hpl_off = pl.hpl_off;
+  a.ud = ud;
+  // value tile staged in LDS: [P][vt] partial rows, vt a multiple of 4 within ~128 KB
+  int vt = (32768 - hsmax - 256) / pmax;
+  vt = vt > 64 ? 64 : (vt & ~3);
+  if (vt < 4) return hipErrorInvalidValue;
+  a.vt = vt;
+  const size_t lds = (size_t)(pmax * vt + hsmax + 256) * sizeof(float);
+  dim3 grid(pl.n_layers + 1, pl.n_chains);
+  const bool gonly = ud.grad_only != 0, xi = ud.xi_hyp || ud.xi_hyp_resample;
+  const bool cyc = ud.schedule == DGPRF_SCHED_CYCLICAL;
+#define DGPRF_HYP(G_, X_, C_)                                                   \
+  do {                                                                         \
+    dgprf::set_lds_limit((const void*)k_step_hyper<G_, X_, C_>, lds);          \
+    hipLaunchKernelGGL((k_step_hyper<G_, X_, C_>), grid, dim3(256), lds, s, a); \
+  } while (0)
+  if (gonly) DGPRF_HYP(true, false, false);
+  else if (xi) {
+    if (cyc) DGPRF_HYP(false, true, true);
+    else DGPRF_HYP(false, true, false);
+  } else {
+    if (cyc) DGPRF_HYP(false, false, true);
+    else DGPRF_HYP(false, false, false);
+  }
+#undef DGPRF_HYP
   return hipGetLastError();
 }
 

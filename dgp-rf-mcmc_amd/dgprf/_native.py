@@ -19,6 +19,10 @@ LIK_GAUSSIAN, LIK_SOFTMAX = 0, 1
 BATCH_DIRECT, BATCH_INDEXED, BATCH_EPOCH = 0, 1, 2
 SCHED_CONST, SCHED_CYCLICAL = 0, 1
 RNG_NOISE, RNG_RESAMPLE, RNG_Z, RNG_W, RNG_MOMENTS = 1, 2, 3, 4, 5
+RNG_HYPER, RNG_HYPER_RESAMPLE = 6, 7
+HYP_KERNEL, HYP_LIK, HYP_MEAN = 1, 2, 4
+HMASS = 32  # hmass slots: log_amp l -> l, log_inv_ls l -> 8 + l, mean l -> 16 + l, lik_log_var -> 24
+ABI_VERSION = 2
 
 E_ARG, E_SHAPE, E_HIP, E_PLAN = -1, -2, -3, -4
 
@@ -36,6 +40,7 @@ class Plan(ctypes.Structure):
         ("n_layers", _i32), ("d_in", _i32), ("d_out", _i32), ("input_cat", _i32),
         ("likelihood", _i32), ("batch", _i32), ("n_chains", _i32),
         ("kind", _i32 * _L), ("n_rf", _i32 * _L), ("n_gp", _i32 * _L),
+        ("hyp_flags", _i32), ("hyp_per_chain", _i32), ("ard", _i32 * _L),
         ("initialised", _i32),
         ("d", _i32 * _L), ("P", _i32 * _L), ("ns", _i32 * _L), ("cpw", _i32 * _L),
         ("n_row_tiles", _i32), ("n_rt_pad", _i32),
@@ -43,7 +48,8 @@ class Plan(ctypes.Structure):
         ("mean_off", _i64 * _L), ("fp_off", _i64 * _L), ("dxp_off", _i64 * _L),
         ("gwp_off", _i64), ("logp_off", _i64),
         ("omega_total", _i64), ("w_total", _i64), ("hyp_total", _i64), ("der_total", _i64),
-        ("ws_chain", _i64), ("ws_total", _i64), ("xb_off", _i64), ("yb_off", _i64),
+        ("ws_chain", _i64), ("ws_total", _i64), ("hpp_off", _i64 * _L), ("hpl_off", _i64),
+        ("xb_off", _i64), ("yb_off", _i64),
         ("yb_cols", _i32), ("pad2", _i32),
     ]
 
@@ -51,6 +57,7 @@ class Plan(ctypes.Structure):
 class Chain(ctypes.Structure):
     """dgprf_chain_t."""
     _fields_ = [("theta", _vp), ("mom", _vp), ("omega", _vp), ("der", _vp), ("mass", _vp),
+                ("z", _vp), ("hyp", _vp), ("hmom", _vp), ("hmass", _vp),
                 ("ws", _vp), ("step", _vp), ("seed", _u64)]
 
 
@@ -66,8 +73,8 @@ class Step(ctypes.Structure):
                 ("temperature", ctypes.c_float), ("data_size", ctypes.c_float),
                 ("resample_moments", _i32), ("schedule", _i32), ("step_offset", _i32),
                 ("grad_only", _i32), ("start_step", _i64), ("cycle_length", _i64),
-                ("resample_in_cycle_head", _i32), ("pad1", _i32), ("xi", _vp),
-                ("xi_resample", _vp)]
+                ("resample_in_cycle_head", _i32), ("full_bayes", _i32), ("xi", _vp),
+                ("xi_resample", _vp), ("xi_hyp", _vp), ("xi_hyp_resample", _vp)]
 
 
 # name -> (restype, argtypes); must match include/dgprf.h exactly.
@@ -80,7 +87,7 @@ SIGNATURES = {
     "dgprf_sghmc_step": (_i32, [ctypes.POINTER(Plan), ctypes.POINTER(Chain),
                                 ctypes.POINTER(Batch), ctypes.POINTER(Step), _vp]),
     "dgprf_potential_grad": (_i32, [ctypes.POINTER(Plan), ctypes.POINTER(Chain),
-                                    ctypes.POINTER(Batch), ctypes.c_float, _vp, _vp]),
+                                    ctypes.POINTER(Batch), ctypes.c_float, _i32, _vp, _vp]),
     "dgprf_graph_create_sghmc": (_i32, [ctypes.POINTER(_vp), ctypes.POINTER(Plan),
                                         ctypes.POINTER(Chain), ctypes.POINTER(Batch),
                                         ctypes.POINTER(Step), _i32]),
@@ -98,8 +105,9 @@ SIGNATURES = {
     "dgprf_prior_w": (_i32, [ctypes.POINTER(Plan), _vp, _vp, _vp]),
     "dgprf_sghmc_update": (_i32, [ctypes.POINTER(Plan), _vp, _vp, _vp, _vp, _vp, _u64,
                                   ctypes.POINTER(Step), _vp]),
-    "dgprf_welford_update": (_i32, [ctypes.POINTER(Plan), _vp, _vp, _vp, _i32, _vp]),
-    "dgprf_mass_estimate": (_i32, [ctypes.POINTER(Plan), _vp, _vp, _i32, _i32, _vp, _vp]),
+    "dgprf_welford_update": (_i32, [ctypes.POINTER(Plan), _vp, _vp, _vp, _i32, _i32, _vp]),
+    "dgprf_mass_estimate": (_i32, [ctypes.POINTER(Plan), _vp, _vp, _i32, _i32, _i32, _vp, _vp,
+                                   _vp]),
 }
 
 _lib = None
@@ -129,7 +137,7 @@ def lib():
         f = getattr(h, name)
         f.restype = res
         f.argtypes = args
-    if h.dgprf_abi_version() != 1:
+    if h.dgprf_abi_version() != ABI_VERSION:
         raise ImportError("libdgprf.so ABI version mismatch")
     _lib = h
     return h
@@ -145,8 +153,11 @@ def call(name, *args):
     return rc
 
 
-def make_plan(d_in, d_out, kinds, n_rf, n_gp, input_cat, likelihood, batch, n_chains):
-    """Fill and derive a Plan (dgprf_plan_init is host-only: usable without a GPU)."""
+def make_plan(d_in, d_out, kinds, n_rf, n_gp, input_cat, likelihood, batch, n_chains,
+              hyp_flags=0, hyp_per_chain=0, ard=None):
+    """Fill and derive a Plan (dgprf_plan_init is host-only: usable without a GPU).
+    hyp_flags: HYP_* groups trainable under full_bayesian=True; ard[l]: per-dimension length
+    scales (the DGP_RF default, models/dgp.py:80-85) or one scalar."""
     L = len(kinds)
     if not 1 <= L <= MAX_LAYERS:
         raise ValueError(f"n_hidden_layers must be in [1, {MAX_LAYERS}]")
@@ -154,7 +165,9 @@ def make_plan(d_in, d_out, kinds, n_rf, n_gp, input_cat, likelihood, batch, n_ch
     p.n_layers, p.d_in, p.d_out = L, int(d_in), int(d_out)
     p.input_cat, p.likelihood = int(bool(input_cat)), int(likelihood)
     p.batch, p.n_chains = int(batch), int(n_chains)
+    p.hyp_flags, p.hyp_per_chain = int(hyp_flags), int(bool(hyp_per_chain))
     for l in range(L):
         p.kind[l], p.n_rf[l], p.n_gp[l] = int(kinds[l]), int(n_rf[l]), int(n_gp[l])
+        p.ard[l] = 1 if ard is None else int(bool(ard[l]))
     call("dgprf_plan_init", ctypes.byref(p))
     return p

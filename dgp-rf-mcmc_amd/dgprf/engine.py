@@ -76,7 +76,8 @@ def normal(shape, purpose, dev=None, out=None):
 class ModelSpec:
     """Static shape of a DGP_RF (the constructor arguments of models/dgp.py:9-52)."""
 
-    def __init__(self, d_in, d_out, kinds, n_rf, n_gp, input_cat=False, likelihood=N.LIK_GAUSSIAN):
+    def __init__(self, d_in, d_out, kinds, n_rf, n_gp, input_cat=False, likelihood=N.LIK_GAUSSIAN,
+                 hyp_flags=N.HYP_KERNEL | N.HYP_LIK, ard=None):
         self.d_in, self.d_out = int(d_in), int(d_out)
         self.kinds = [int(k) for k in kinds]
         self.n_rf = [int(r) for r in n_rf]
@@ -84,28 +85,42 @@ class ModelSpec:
         self.input_cat = bool(input_cat)
         self.likelihood = int(likelihood)
         self.L = len(self.kinds)
+        # full_bayesian=True: which hyper-parameter groups are trainable, ARD per layer
+        self.hyp_flags = int(hyp_flags)
+        self.ard = [1] * self.L if ard is None else [int(bool(a)) for a in ard]
 
-    def plan(self, batch=1, n_chains=1):
+    def plan(self, batch=1, n_chains=1, hyp_per_chain=False):
         return N.make_plan(self.d_in, self.d_out, self.kinds, self.n_rf, self.n_gp,
-                           self.input_cat, self.likelihood, batch, n_chains)
+                           self.input_cat, self.likelihood, batch, n_chains, self.hyp_flags,
+                           hyp_per_chain, self.ard)
 
 
 class Engine:
-    def __init__(self, spec, n_chains=1, dev=None, seed=None):
+    def __init__(self, spec, n_chains=1, dev=None, seed=None, per_chain_hyp=None):
+        """per_chain_hyp: every chain owns its kernel / likelihood hyper-parameters (and Omega),
+        needed to sample them with full_bayesian=True across several chains; default: only when
+        C == 1 (where it changes nothing), i.e. C > 1 chains share one hyper-parameter set."""
         self.spec = spec
         self.C = int(n_chains)
         self.dev = dev or device()
-        self.layout = spec.plan(1, self.C)
+        self.per_chain_hyp = (self.C == 1) if per_chain_hyp is None else bool(per_chain_hyp)
+        self.layout = spec.plan(1, self.C, self.per_chain_hyp)
         pl = self.layout
         self.L = spec.L
         f = lambda n: torch.zeros(int(n), dtype=_F32, device=self.dev)
+        Ch = self.C if self.per_chain_hyp else 1
         self.theta = torch.zeros(self.C, pl.w_total, dtype=_F32, device=self.dev)
         self.mom = torch.zeros(self.C, pl.w_total, dtype=_F32, device=self.dev)
         self.mass = torch.ones(self.C, self.L, dtype=_F32, device=self.dev)
         self.z = f(max(pl.omega_total, 1))
-        self.omega = f(max(pl.omega_total, 1))
-        self.hyp = f(pl.hyp_total)
-        self.der = f(pl.der_total)
+        # chain 0 first: the views below address chain 0 (the reference's single model)
+        self.omega = f(max(pl.omega_total, 1) * Ch)
+        self.hyp = f(pl.hyp_total * Ch)
+        self.der = f(pl.der_total * Ch)
+        # full_bayesian=True: hyper-parameter momenta (hyp layout) and masses (N.HMASS slots)
+        self.hmom = torch.zeros(self.C, pl.hyp_total, dtype=_F32, device=self.dev)
+        self.hmass = torch.ones(self.C, N.HMASS, dtype=_F32, device=self.dev)
+        self.hyper_moments_ready = False
         self.step_ctr = torch.zeros(1, dtype=torch.int64, device=self.dev)
         self.seed = _RNG.seed if seed is None else int(seed)
         self.lik_log_var_source = None  # callable -> device scalar tensor (Gaussian likelihood)
@@ -159,28 +174,46 @@ class Engine:
         for l in range(self.L):
             self.lis_view(l).fill_(-0.5 * math.log(self.layout.d[l]))  # kernels/RBF.py:16-17,40
 
-    def init_moments(self):
-        """param.M = 1, param.moments ~ N(0,1) (models/dgp.py:235-240)."""
+    def init_moments(self, hyper=False):
+        """param.M = 1, param.moments ~ N(0,1) (models/dgp.py:235-240); hyper=True also for the
+        kernel / likelihood hyper-parameters (full_bayesian=True, vars = trainable_variables)."""
         self.mass.fill_(1.0)
         normal(None, N.RNG_MOMENTS, out=self.mom)
         self.moments_ready = True
+        if hyper:
+            self.init_hyper_moments()
+
+    def init_hyper_moments(self):
+        self.hmass.fill_(1.0)
+        normal(None, N.RNG_MOMENTS, out=self.hmom)
+        self.hyper_moments_ready = True
+
+    def hyp_chain(self, chain):
+        """[hyp_total] hyper-parameters of `chain` (the shared set when not per chain)."""
+        pl = self.layout
+        c = chain if self.per_chain_hyp else 0
+        return self.hyp[c * pl.hyp_total:(c + 1) * pl.hyp_total]
 
     # ---------------------------------------------------------------- per-B plans
     def plan_ws(self, B):
         B = int(B)
         if B not in self._ws:
-            pl = self.spec.plan(B, self.C)
+            pl = self.spec.plan(B, self.C, self.per_chain_hyp)
             ws = torch.zeros(max(pl.ws_total, 4), dtype=_F32, device=self.dev)
             self._ws[B] = (pl, ws)
         return self._ws[B]
 
-    def chain_struct(self, ws, omega=None):
+    def chain_struct(self, ws, omega=None, z=None):
         c = N.Chain()
         c.theta = self.theta.data_ptr()
         c.mom = self.mom.data_ptr()
         c.omega = (self.omega if omega is None else omega).data_ptr()
         c.der = self.der.data_ptr()
         c.mass = self.mass.data_ptr()
+        c.z = (self.z if z is None else z).data_ptr()
+        c.hyp = self.hyp.data_ptr()
+        c.hmom = self.hmom.data_ptr()
+        c.hmass = self.hmass.data_ptr()
         c.ws = ws.data_ptr()
         c.step = self.step_ctr.data_ptr()
         c.seed = self.seed
@@ -201,7 +234,7 @@ class Engine:
     @staticmethod
     def step_struct(lr, beta, T, data_size, resample=False, schedule=N.SCHED_CONST,
                     start_step=0, cycle_length=1, resample_head=False, xi=None, xi_resample=None,
-                    step_offset=0):
+                    step_offset=0, full_bayes=False, xi_hyp=None, xi_hyp_resample=None):
         s = N.Step()
         s.lr, s.momentum_decay, s.temperature = float(lr), float(beta), float(T)
         s.data_size = float(data_size)
@@ -213,6 +246,9 @@ class Engine:
         s.resample_in_cycle_head = int(bool(resample_head))
         s.xi = xi.data_ptr() if xi is not None else None
         s.xi_resample = xi_resample.data_ptr() if xi_resample is not None else None
+        s.full_bayes = int(bool(full_bayes))
+        s.xi_hyp = xi_hyp.data_ptr() if xi_hyp is not None else None
+        s.xi_hyp_resample = xi_hyp_resample.data_ptr() if xi_hyp_resample is not None else None
         return s
 
     # ---------------------------------------------------------------- hyper-params
@@ -251,39 +287,56 @@ class Engine:
         bt = self.batch_struct(X, Y, mode, idx, iters, perm_seed)
         return pl, ws, bt, (X, Y, idx)
 
+    def _check_full_bayes(self):
+        if not self.hyper_moments_ready:
+            raise AssertionError("Trainable Params do not have attr moments!")  # dgp.py:208
+        if self.C > 1 and not self.per_chain_hyp:
+            raise ValueError("full_bayesian=True with several chains needs per_chain_hyp=True")
+
     def step(self, X, Y, data_size, lr, beta, T, resample=False, xi=None, xi_resample=None,
              build=True, omega=None, batch_size=None, mode=N.BATCH_DIRECT, idx=None,
-             perm_seed=0):
-        """One sgmcmc_update (default: X, Y are the batch, DGPRF_BATCH_DIRECT)."""
+             perm_seed=0, full_bayes=False, xi_hyp=None, xi_hyp_resample=None, z=None):
+        """One sgmcmc_update (default: X, Y are the batch, DGPRF_BATCH_DIRECT).
+        full_bayes: also update the trainable hyper-parameters (models/dgp.py:199-216); Omega,
+        c and sigma^2 are rebuilt on the device afterwards."""
+        if full_bayes:
+            self._check_full_bayes()
         pl, ws, bt, keep = self._batch(X, Y, batch_size, mode, idx, perm_seed)
         if build:
             self.build_omega()
-        ch = self.chain_struct(ws, omega)
-        xi = None if xi is None else as_device(xi, self.dev)
-        xr = None if xi_resample is None else as_device(xi_resample, self.dev)
-        st = self.step_struct(lr, beta, T, data_size, resample, xi=xi, xi_resample=xr)
+        ch = self.chain_struct(ws, omega, z)
+        dv = lambda t: None if t is None else as_device(t, self.dev)
+        xi, xr, xh, xhr = dv(xi), dv(xi_resample), dv(xi_hyp), dv(xi_hyp_resample)
+        st = self.step_struct(lr, beta, T, data_size, resample, xi=xi, xi_resample=xr,
+                              full_bayes=full_bayes, xi_hyp=xh, xi_hyp_resample=xhr)
         N.call("dgprf_sghmc_step", ctypes.byref(pl), ctypes.byref(ch), ctypes.byref(bt),
                ctypes.byref(st), stream())
 
     def grad(self, X, Y, data_size, build=True, omega=None, batch_size=None,
-             mode=N.BATCH_DIRECT, idx=None, perm_seed=0):
-        """dU/dW for every layer and chain -> [C, w_total] (dgprf_potential_grad)."""
+             mode=N.BATCH_DIRECT, idx=None, perm_seed=0, full_bayes=False, z=None):
+        """dU/dW for every layer and chain -> [C, w_total] (dgprf_potential_grad); full_bayes:
+        w.r.t. every trainable variable -> [C, w_total + hyp_total] (hyp layout after W)."""
+        if full_bayes and self.C > 1 and not self.per_chain_hyp:
+            raise ValueError("full_bayesian=True with several chains needs per_chain_hyp=True")
         pl, ws, bt, keep = self._batch(X, Y, batch_size, mode, idx, perm_seed)
         if build:
             self.build_omega()
-        out = torch.empty(self.C, self.layout.w_total, dtype=_F32, device=self.dev)
-        ch = self.chain_struct(ws, omega)
+        n = self.layout.w_total + (self.layout.hyp_total if full_bayes else 0)
+        out = torch.empty(self.C, n, dtype=_F32, device=self.dev)
+        ch = self.chain_struct(ws, omega, z)
         N.call("dgprf_potential_grad", ctypes.byref(pl), ctypes.byref(ch), ctypes.byref(bt),
-               float(data_size), ptr(out), stream())
+               float(data_size), int(bool(full_bayes)), ptr(out), stream())
         return out
 
     def graph(self, X_all, Y_all, batch_size, data_size, lr, beta, T, steps_per_graph,
               schedule=N.SCHED_CONST, start_step=0, cycle_length=1, resample_head=False,
-              perm_seed=0):
+              perm_seed=0, full_bayes=False):
         """hipGraph of `steps_per_graph` on-device-minibatched steps (DGPRF_BATCH_EPOCH)."""
+        if full_bayes:
+            self._check_full_bayes()
         key = (X_all.data_ptr(), Y_all.data_ptr(), int(batch_size), float(data_size), float(lr),
                float(beta), float(T), int(steps_per_graph), int(schedule), int(start_step),
-               int(cycle_length), bool(resample_head), int(perm_seed))
+               int(cycle_length), bool(resample_head), int(perm_seed), bool(full_bayes))
         if key in self._graphs:
             return self._graphs[key]
         pl, ws = self.plan_ws(batch_size)
@@ -291,7 +344,7 @@ class Engine:
         ch = self.chain_struct(ws)
         bt = self.batch_struct(X_all, Y_all, N.BATCH_EPOCH, iters=iters, perm_seed=perm_seed)
         st = self.step_struct(lr, beta, T, data_size, False, schedule, start_step, cycle_length,
-                              resample_head)
+                              resample_head, full_bayes=full_bayes)
         h = ctypes.c_void_p()
         N.call("dgprf_graph_create_sghmc", ctypes.byref(h), ctypes.byref(pl), ctypes.byref(ch),
                ctypes.byref(bt), ctypes.byref(st), int(steps_per_graph))
@@ -367,14 +420,31 @@ class Engine:
         return out
 
     # ---------------------------------------------------------------- preconditioner
-    def welford(self, grad, mean, m2, k):
+    def welford(self, grad, mean, m2, k, full_bayes=False):
         N.call("dgprf_welford_update", ctypes.byref(self.layout), ptr(grad), ptr(mean), ptr(m2),
-               int(k), stream())
+               int(k), int(bool(full_bayes)), stream())
 
-    def mass_estimate(self, mean, m2, K, centered):
+    def mass_estimate(self, mean, m2, K, centered, full_bayes=False):
+        """W masses [C, L]; full_bayes: also (hyper masses [C, N.HMASS])."""
         out = torch.empty(self.C, self.L, dtype=_F32, device=self.dev)
+        hout = torch.zeros(self.C, N.HMASS, dtype=_F32, device=self.dev) if full_bayes else None
         N.call("dgprf_mass_estimate", ctypes.byref(self.layout), ptr(mean), ptr(m2), int(K),
-               int(bool(centered)), ptr(out), stream())
+               int(bool(centered)), int(bool(full_bayes)), ptr(out), ptr(hout), stream())
+        return (out, hout) if full_bayes else out
+
+    def hyper_slots(self):
+        """The trainable hyper-parameter variables of full_bayesian=True as
+        (hmass slot, hyp offset, length) — log_amp, log_inv_ls, mean per layer, then lik_log_var."""
+        pl, sp = self.layout, self.spec
+        out = []
+        for l in range(self.L):
+            if sp.hyp_flags & N.HYP_KERNEL:
+                out.append((l, l, 1))
+                out.append((8 + l, pl.lis_off[l], pl.d[l] if sp.ard[l] else 1))
+            if sp.hyp_flags & N.HYP_MEAN:
+                out.append((16 + l, pl.mean_off[l], pl.d[l]))
+        if (sp.hyp_flags & N.HYP_LIK) and sp.likelihood == N.LIK_GAUSSIAN:
+            out.append((24, self.L, 1))
         return out
 
     def sghmc_update(self, grad, lr, beta, T, data_size, resample=False, xi=None,

@@ -114,8 +114,18 @@ class DGP_RF(Module):
     def _bind_engine(self):
         """Pack every layer's state into one Engine and rebind the objects to views of it."""
         kinds = [N.RBF if k == 'RBF' else N.ARC for k in self.kernel_type_list]
+        # trainable hyper-parameter groups of full_bayesian=True (models/dgp.py:175-181)
+        flags = 0
+        if self.kernel_trainable:
+            flags |= N.HYP_KERNEL
+        if self.set_nonzero_mean:
+            flags |= N.HYP_MEAN
+        if isinstance(self.likelihood, Gaussian) and \
+                getattr(self.likelihood.lik_log_var, "trainable", True):
+            flags |= N.HYP_LIK
         spec = E.ModelSpec(self.d_in, self.d_out, kinds, self.n_rf, self.n_gp, self.input_cat,
-                           self._lik_code())
+                           self._lik_code(), hyp_flags=flags,
+                           ard=[int(k.is_ard) for k in self.kernel_list])
         eng = E.Engine(spec, n_chains=1)
         for l in range(self.n_hidden_layers):
             rf, gp, k = self.BNN.layers[2 * l], self.BNN.layers[2 * l + 1], self.kernel_list[l]
@@ -126,6 +136,9 @@ class DGP_RF(Module):
         self._engine = eng
         self._rebind_z()
         if isinstance(self.likelihood, Gaussian):
+            # bound to its engine slot: full_bayesian=True updates it on the device
+            self.likelihood.lik_log_var = rebind(self.likelihood.lik_log_var,
+                                                 eng.lik_log_var_view())
             eng.lik_log_var_source = lambda: self.likelihood.lik_log_var
         self.BNN._model = self
 
@@ -173,6 +186,23 @@ class DGP_RF(Module):
         om = torch.empty_like(eng.omega)
         eng.build_omega(z=z, omega=om)
         return om
+
+    def _omega_and_z_for_call(self):
+        """Like _omega_for_call, also returning the z that built Omega (full_bayesian=True
+        differentiates through Omega = exp(lis) z + mean with that z)."""
+        eng = self._engine
+        fresh = [l for l in range(self.n_hidden_layers) if not self.BNN.layers[2 * l].random_fixed]
+        if not fresh:
+            eng.build_omega()
+            return None, None
+        z = eng.z.clone()
+        for l in fresh:
+            pl = eng.layout
+            o, n = pl.omega_off[l], pl.d[l] * pl.n_rf[l]
+            E.normal(None, N.RNG_Z, out=z[o:o + n])
+        om = torch.empty_like(eng.omega)
+        eng.build_omega(z=z, omega=om)
+        return om, z
 
     def _fused_forward(self, X):
         om = self._omega_for_call()
@@ -225,65 +255,94 @@ class DGP_RF(Module):
         return -(prior + ll)
 
     # ------------------------------------------------------------------ sampler
-    def _check_moments(self):
-        if not self._engine.moments_ready:
+    def _check_moments(self, full_bayesian=False):
+        eng = self._engine
+        if not eng.moments_ready or (full_bayesian and not eng.hyper_moments_ready):
             raise AssertionError("Trainable Params do not have attr moments!")  # dgp.py:208
 
-    def _attach_sampler_attrs(self):
+    def _hyper_vars(self):
+        """(variable, hmass slot, hyp offset, length) of every trainable hyper-parameter."""
+        eng = self._engine
+        by_off = {}
+        for l in range(self.n_hidden_layers):
+            k, rf = self.kernel_list[l], self.BNN.layers[2 * l]
+            by_off[l] = k.log_amplitude
+            by_off[eng.layout.lis_off[l]] = k.log_inv_length_scale
+            by_off[eng.layout.mean_off[l]] = rf.mean
+        if isinstance(self.likelihood, Gaussian):
+            by_off[self.n_hidden_layers] = self.likelihood.lik_log_var
+        return [(by_off[o], slot, o, n) for slot, o, n in eng.hyper_slots()]
+
+    def _attach_sampler_attrs(self, full_bayesian=False):
         eng = self._engine
         for l, W in enumerate(self.W_mcmc):
             W.moments = eng.mom_view(l)
             W.M = eng.mass[0, l]
+        if full_bayesian:
+            for v, slot, o, n in self._hyper_vars():
+                v.moments = eng.hmom[0, o:o + n].view(v.shape)
+                v.M = eng.hmass[0, slot]
 
     def sgmcmc_update(self, X_batch, Y_batch, data_size, lr=0.01, momentum_decay=0.95,
                       resample_moments=False, temperature=1., full_bayesian=False):
         """One SGHMC (SGLD when momentum_decay = 0) step for W (models/dgp.py:184-216):
         m <- b m - h N dU/dW + sqrt(2(1-b) T M) xi,  W <- W + h m / M,  h = sqrt(lr / N).
         Runs as one fused forward/backward/update sequence of HIP kernels."""
-        if full_bayesian:
-            raise NotImplementedError(
-                "full_bayesian=True (gradients w.r.t. kernel/likelihood hyper-parameters, "
-                "models/dgp.py:175-181,199-204) is not implemented by the HIP engine yet")
-        self._check_moments()
-        om = self._omega_for_call()
+        self._check_moments(full_bayesian)
+        om, z = self._omega_and_z_for_call()
         self._engine.step(X_batch, Y_batch, data_size, lr, momentum_decay, temperature,
-                          bool(resample_moments), build=False, omega=om)
+                          bool(resample_moments), build=False, omega=om, z=z,
+                          full_bayes=bool(full_bayesian))
 
     def precond_update(self, ds, data_size, K_batches=32, full_bayesian=False,
                        precond_type='rmsprop', second_moment_centered=False):
         """Preconditioner M per W_l from K minibatch gradients (models/dgp.py:218-299):
         Welford mean/M2 on the device, mass = sqrt(mean(E[g^2]) + 1e-7) (or the centred
         variance), normalised by the smallest mass; momenta rescaled by sqrt(M)."""
-        if full_bayesian:
-            raise NotImplementedError(
-                "full_bayesian=True preconditioning is not implemented by the HIP engine yet")
         eng = self._engine
         if not eng.moments_ready:
             eng.init_moments()
             self._attach_sampler_attrs()
+        if full_bayesian and not eng.hyper_moments_ready:
+            eng.init_hyper_moments()  # vars = self.trainable_variables (models/dgp.py:230-240)
+            self._attach_sampler_attrs(full_bayesian=True)
         if precond_type == 'identity':
             return None
         elif precond_type == 'rmsprop':
             L = self.n_hidden_layers
+            hv = self._hyper_vars() if full_bayesian else []
             m_c = [torch.rsqrt(eng.mass[0, l]) * eng.mom_view(l) for l in range(L)]
-            mean = torch.zeros_like(eng.theta)
-            m2 = torch.zeros_like(eng.theta)
-            om = self._omega_for_call()
+            m_ch = [torch.rsqrt(eng.hmass[0, slot]) * eng.hmom[0, o:o + n]
+                    for _, slot, o, n in hv]
+            n_all = eng.layout.w_total + (eng.layout.hyp_total if full_bayesian else 0)
+            mean = torch.zeros(eng.C, n_all, dtype=torch.float32, device=eng.dev)
+            m2 = torch.zeros_like(mean)
+            om, z = self._omega_and_z_for_call()
             k = 0
             for X_batch, Y_batch in ds:
-                g = eng.grad(X_batch, Y_batch, data_size, build=False, omega=om)
+                g = eng.grad(X_batch, Y_batch, data_size, build=False, omega=om, z=z,
+                             full_bayes=bool(full_bayesian))
                 k = k + 1
-                eng.welford(g, mean, m2, k)
+                eng.welford(g, mean, m2, k, full_bayes=bool(full_bayesian))
                 if k == K_batches:
                     break
             assert k == K_batches, \
                 f"Estimating M ends before we use {K_batches} batches, we actually use {k} batches!"
-            mass_est = eng.mass_estimate(mean, m2, K_batches, second_moment_centered)
+            est = eng.mass_estimate(mean, m2, K_batches, second_moment_centered,
+                                    full_bayes=bool(full_bayesian))
+            mass_est, hmass_est = (est if full_bayesian else (est, None))
             self._mass_estimate = mass_est[0]
+            # scale the minimum estimated mass (over every variable) to one (dgp.py:289-296)
             mass_min = torch.min(mass_est[0])
+            if hv:
+                slots = torch.tensor([slot for _, slot, _, _ in hv], device=eng.dev)
+                mass_min = torch.minimum(mass_min, torch.min(hmass_est[0, slots]))
             eng.mass.copy_(mass_est / mass_min)
             for l in range(L):
                 eng.mom_view(l).copy_(torch.sqrt(eng.mass[0, l]) * m_c[l])
+            for (_, slot, o, n), mc in zip(hv, m_ch):
+                eng.hmass[0, slot] = hmass_est[0, slot] / mass_min
+                eng.hmom[0, o:o + n] = torch.sqrt(eng.hmass[0, slot]) * mc
             return None
         else:
             raise NotImplementedError
@@ -296,12 +355,14 @@ class DGP_RF(Module):
     # ------------------------------------------------------------------ engine-path sampling
     def run_sgmcmc(self, X_all, Y_all, data_size, n_steps, batch_size=200, lr=0.01,
                    momentum_decay=0.9, temperature=1., steps_per_graph=50, perm_seed=0,
-                   schedule=None, start_step=0, cycle_length=1, resample_in_cycle_head=False):
+                   schedule=None, start_step=0, cycle_length=1, resample_in_cycle_head=False,
+                   full_bayesian=False):
         """Run n_steps sgmcmc_update steps with device-resident data: per-epoch shuffled,
         drop-remainder minibatches (experiments/utils_dataset.py:38-42) drawn on the device and
         `steps_per_graph` steps per hipGraph replay.  schedule='cyclical' applies the driver's
-        burn-in + cosine schedule on the device (experiments/utils_training.py:41-61)."""
-        self._check_moments()
+        burn-in + cosine schedule on the device (experiments/utils_training.py:41-61).
+        full_bayesian=True also samples the trainable hyper-parameters (models/dgp.py:199-204)."""
+        self._check_moments(full_bayesian)
         eng = self._engine
         if not all(self.BNN.layers[2 * l].random_fixed for l in range(self.n_hidden_layers)):
             raise NotImplementedError("run_sgmcmc needs random_fixed=True")
@@ -313,11 +374,13 @@ class DGP_RF(Module):
         sched = N.SCHED_CYCLICAL if schedule == 'cyclical' else N.SCHED_CONST
         spg = max(1, min(int(steps_per_graph), int(n_steps)))
         g = eng.graph(X_all, Y_all, batch_size, data_size, lr, momentum_decay, temperature, spg,
-                      sched, start_step, cycle_length, resample_in_cycle_head, perm_seed)
+                      sched, start_step, cycle_length, resample_in_cycle_head, perm_seed,
+                      full_bayes=bool(full_bayesian))
         full, rest = divmod(int(n_steps), spg)
         for _ in range(full):
             g.launch()
         if rest:
             g2 = eng.graph(X_all, Y_all, batch_size, data_size, lr, momentum_decay, temperature,
-                           rest, sched, start_step, cycle_length, resample_in_cycle_head, perm_seed)
+                           rest, sched, start_step, cycle_length, resample_in_cycle_head, perm_seed,
+                           full_bayes=bool(full_bayesian))
             g2.launch()

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define DGPRF_ABI_VERSION 1
+#define DGPRF_ABI_VERSION 2
 
 #define DGPRF_MAX_LAYERS 8
 #define DGPRF_MAX_G 64        /* max latent GPs per layer (n_gp[l]) */
@@ -54,6 +54,20 @@ extern "C" {
 #define DGPRF_RNG_Z 3          /* z ~ N(0,1) RF frequencies       (layers/rf_layers.py:22) */
 #define DGPRF_RNG_W 4          /* W ~ N(0,1) GP weights           (layers/GP_weight_layers.py:9) */
 #define DGPRF_RNG_MOMENTS 5    /* initial momenta                 (models/dgp.py:240) */
+#define DGPRF_RNG_HYPER 6      /* xi of the hyper-parameter updates (full_bayesian=True) */
+#define DGPRF_RNG_HYPER_RESAMPLE 7 /* resampled hyper-parameter momenta          */
+
+/* Trainable hyper-parameter groups of full_bayesian=True (plan.hyp_flags; models/dgp.py:175-181,
+ * 199-204): the kernels' log_amplitude and log_inv_length_scale (kernel_trainable,
+ * kernels/RBF.py:39-41), the layer means (set_nonzero_mean, layers/rf_layers.py:23-26) and the
+ * Gaussian lik_log_var (likelihoods/gaussian.py:12). */
+#define DGPRF_HYP_KERNEL 1
+#define DGPRF_HYP_LIK 2
+#define DGPRF_HYP_MEAN 4
+/* Hyper-parameter masses per chain (dgprf_chain_t.hmass [C][DGPRF_HMASS]): log_amp of layer l at
+ * l, log_inv_ls at 8 + l, mean at 16 + l, lik_log_var at 24 (one mass per tf.Variable, like the
+ * reference's param.M). */
+#define DGPRF_HMASS 32
 
 /* error codes */
 #define DGPRF_OK 0
@@ -90,6 +104,9 @@ typedef struct dgprf_plan {
   int32_t kind[DGPRF_MAX_LAYERS];
   int32_t n_rf[DGPRF_MAX_LAYERS];
   int32_t n_gp[DGPRF_MAX_LAYERS];
+  int32_t hyp_flags;       /* DGPRF_HYP_* groups that are trainable (full_bayesian=True) */
+  int32_t hyp_per_chain;   /* 1: hyp / omega / der are per chain ([C][...]); 0: shared */
+  int32_t ard[DGPRF_MAX_LAYERS]; /* 1: per-dimension log_inv_ls; 0: one scalar (d equal slots) */
   /* ---- derived by dgprf_plan_init ---- */
   int32_t initialised;
   int32_t d[DGPRF_MAX_LAYERS];      /* layer input width */
@@ -112,6 +129,8 @@ typedef struct dgprf_plan {
   int64_t der_total;
   int64_t ws_chain;
   int64_t ws_total;
+  int64_t hpp_off[DGPRF_MAX_LAYERS]; /* full-Bayes partials [n_rt_pad][16][align4(2 d_l + 1)] (per chain) */
+  int64_t hpl_off;                   /* full-Bayes lik_log_var partials [n_rt_pad] (per chain)  */
   int64_t xb_off;                    /* gathered minibatch rows X [B][d_in] (per chain)        */
   int64_t yb_off;                    /* gathered minibatch targets [B][yb_cols] (per chain)    */
   int32_t yb_cols;                   /* g_L (Gaussian) or 1 (softmax label)                    */
@@ -123,9 +142,14 @@ typedef struct dgprf_plan {
 typedef struct dgprf_chain {
   float *theta;          /* [C][w_total] */
   float *mom;            /* [C][w_total] */
-  const float *omega;    /* [omega_total] (from dgprf_omega_build) */
-  const float *der;      /* [der_total]   (from dgprf_omega_build) */
+  float *omega;          /* [omega_total] or [C][omega_total] (from dgprf_omega_build) */
+  float *der;            /* [der_total] or [C][der_total]     (from dgprf_omega_build) */
   const float *mass;     /* [C][n_layers] */
+  /* full_bayesian=True state (may be NULL otherwise): */
+  const float *z;        /* [omega_total] RF base frequencies (Omega is rebuilt after updates) */
+  float *hyp;            /* [hyp_total] or [C][hyp_total] */
+  float *hmom;           /* [C][hyp_total] hyper-parameter momenta (hyp layout) */
+  const float *hmass;    /* [C][DGPRF_HMASS] */
   float *ws;             /* [ws_total] */
   int64_t *step;         /* device step counter (Philox counter / minibatch position) */
   uint64_t seed;         /* Philox key (already folded with the rank by the host) */
@@ -158,10 +182,12 @@ typedef struct dgprf_step {
   int64_t start_step;       /* first sampling step (start_sampling_epoch * iters) */
   int64_t cycle_length;     /* epochs_per_cycle * iters */
   int32_t resample_in_cycle_head;
-  int32_t pad1;
+  int32_t full_bayes;       /* full_bayesian=True: also update the plan.hyp_flags groups */
   /* optional injected standard normals (parity tests; NULL = device Philox): */
   const float *xi;          /* [C][w_total] noise */
   const float *xi_resample; /* [C][w_total] resampled momenta */
+  const float *xi_hyp;          /* [C][hyp_total] hyper-parameter noise (hyp layout) */
+  const float *xi_hyp_resample; /* [C][hyp_total] resampled hyper-parameter momenta */
 } dgprf_step_t;
 
 typedef struct dgprf_graph *dgprf_graph_handle;
@@ -184,21 +210,25 @@ int dgprf_philox_normal(float *out, int64_t n, uint64_t seed, uint64_t subsequen
  * Replaces kernels/RBF.py:43-53, kernels/arc_cosine.py:46-56, layers/rf_layers.py:34-38,44,90,
  * likelihoods/gaussian.py:14-16. */
 int dgprf_omega_build(const dgprf_plan_t *plan, const float *z, const float *hyp, float *omega,
-                      float *der, void *stream);
+                      float *der, void *stream);  /* hyp_per_chain: every chain's [C][...] */
 
 /* ---------------- the hot path ---------------- */
 /* One full SGHMC/SGLD step for every chain: minibatch gather, forward through all L layers
  * (Omega x -> cos|sin or relu -> Phi W), likelihood, analytic backward (gW_l = Phi_l^T dF_l +
  * W_l/N), and the fused update with device Philox noise.  Advances *chain.step by one.
- * Replaces DGP_RF.sgmcmc_update (models/dgp.py:184-216) with full_bayesian=False. */
+ * Replaces DGP_RF.sgmcmc_update (models/dgp.py:184-216); step.full_bayes = full_bayesian=True:
+ * the plan.hyp_flags hyper-parameters take the same update from their gradients (needs chain.z,
+ * hyp, hmom, hmass) and Omega / c / sigma^2 are rebuilt after it. */
 int dgprf_sghmc_step(const dgprf_plan_t *plan, const dgprf_chain_t *chain,
                      const dgprf_batch_t *batch, const dgprf_step_t *step, void *stream);
 
 /* Gradient of U w.r.t. every W_l (models/dgp.py:161-182 + tape.gradient :194-198) into
- * grad_out [C][w_total]; no update, step counter untouched. */
+ * grad_out [C][w_total]; full_bayes: w.r.t. every trainable variable (:175-181, 199-204) into
+ * grad_out [C][w_total + hyp_total] (hyper-parameter gradients in the hyp layout; a scalar
+ * length scale's gradient is written to all d of its slots).  No update, step counter untouched. */
 int dgprf_potential_grad(const dgprf_plan_t *plan, const dgprf_chain_t *chain,
-                         const dgprf_batch_t *batch, float data_size, float *grad_out,
-                         void *stream);
+                         const dgprf_batch_t *batch, float data_size, int32_t full_bayes,
+                         float *grad_out, void *stream);
 
 /* Capture `steps_per_graph` consecutive dgprf_sghmc_step calls (sub-step k uses
  * step_offset = k, then *step += steps_per_graph) into one hipGraph. */
@@ -228,7 +258,8 @@ int dgprf_profile_step(const dgprf_plan_t *plan, const dgprf_chain_t *chain,
  *   se        [C][n]        mean_k (y - f)^2 (Gaussian only)
  *   lse_m/lse_s/se_sum [C][n]  online log-sum-exp over samples (experiments/utils_training.py:79-85)
  *                         updated in place: m' = max(m, lp); s' = s e^{m-m'} + e^{lp-m'}.
- * Y may be NULL when no likelihood output is requested. */
+ * Y may be NULL when no likelihood output is requested.  omega/der are [C][...] when
+ * plan.hyp_per_chain (chain c scored with its own hyper-parameters). */
 int dgprf_forward(const dgprf_plan_t *plan, const float *theta, const float *omega,
                   const float *der, const float *X, const float *Y, int32_t y_cols, int64_t n,
                   float *const *f_out, float *logp, float *se, float *lse_m, float *lse_s,
@@ -266,13 +297,15 @@ int dgprf_sghmc_update(const dgprf_plan_t *plan, float *theta, float *mom, const
                        const float *mass, const int64_t *step_ctr, uint64_t seed,
                        const dgprf_step_t *step, void *stream);
 /* Welford accumulation of one gradient sample (models/dgp.py:259-271):
- * k is the 1-based sample index; mean/m2 [C][w_total]. */
+ * k is the 1-based sample index; grad/mean/m2 [C][w_total] (full_bayes: [C][w_total + hyp_total]). */
 int dgprf_welford_update(const dgprf_plan_t *plan, const float *grad, float *mean, float *m2,
-                         int32_t k, void *stream);
-/* Per-layer mass estimate (models/dgp.py:276-288) into mass_est [C][L]:
+                         int32_t k, int32_t full_bayes, void *stream);
+/* Mass estimate per variable (models/dgp.py:276-288): W_l into mass_est [C][L]; full_bayes: also
+ * the trainable hyper-parameter variables into hmass_est [C][DGPRF_HMASS] (other slots 0).
  * centered: sqrt(mean(m2/(K-1)) + 1e-7); else sqrt(mean(mean^2 + m2/K) + 1e-7). */
 int dgprf_mass_estimate(const dgprf_plan_t *plan, const float *mean, const float *m2,
-                        int32_t k_batches, int32_t centered, float *mass_est, void *stream);
+                        int32_t k_batches, int32_t centered, int32_t full_bayes, float *mass_est,
+                        float *hmass_est, void *stream);
 
 #ifdef __cplusplus
 }

@@ -430,7 +430,7 @@ def test_api_errors(dev):
     with pytest.raises(AssertionError, match="moments"):
         m.sgmcmc_update(X, Y, 100)
     m.precond_update(None, 100, precond_type="identity")
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(AssertionError, match="moments"):   # hyper-parameters have no moments yet
         m.sgmcmc_update(X, Y, 100, full_bayesian=True)
     with pytest.raises(ValueError):
         m.sgmcmc_update(np.zeros((4, 2), np.float32), Y, 100)
