@@ -1057,7 +1057,18 @@ __global__ __launch_bounds__(256) void k_step_hyper(const HypK a) {
     return hyp[slot] + (h * (1.0f / M)) * mn;
   };
   if (blk == L) {  // Gaussian lik_log_var
-    if ((a.flags & DGPRF_HYP_LIK) && a.likelihood == DGPRF_LIK_GAUSSIAN && tid == 0) {
+    const bool lik_tr = (a.flags & DGPRF_HYP_LIK) && a.likelihood == DGPRF_LIK_GAUSSIAN;
+    if (GONLY) {  // slots no block owns (padding, groups that do not train) read as 0
+      for (int64_t s = tid; s < a.hyp_total; s += 256) {
+        bool owned = s < L ? (a.flags & DGPRF_HYP_KERNEL) != 0 : (s == L && lik_tr);
+        for (int q = 0; q < L; ++q) {
+          owned |= (a.flags & DGPRF_HYP_KERNEL) && s >= a.lis_off[q] && s < a.lis_off[q] + a.d[q];
+          owned |= (a.flags & DGPRF_HYP_MEAN) && s >= a.mean_off[q] && s < a.mean_off[q] + a.d[q];
+        }
+        if (!owned) a.grad_out[(int64_t)chain * a.grad_cs + a.w_total + s] = 0.f;
+      }
+    }
+    if (lik_tr && tid == 0) {
       const float* hpl = a.ws + (int64_t)chain * a.ws_cs + a.hpl_off;
       float s = 0.f;
       for (int rt = 0; rt < a.n_rt; ++rt) s += hpl[rt];

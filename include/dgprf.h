@@ -225,7 +225,8 @@ int dgprf_sghmc_step(const dgprf_plan_t *plan, const dgprf_chain_t *chain,
 /* Gradient of U w.r.t. every W_l (models/dgp.py:161-182 + tape.gradient :194-198) into
  * grad_out [C][w_total]; full_bayes: w.r.t. every trainable variable (:175-181, 199-204) into
  * grad_out [C][w_total + hyp_total] (hyper-parameter gradients in the hyp layout; a scalar
- * length scale's gradient is written to all d of its slots).  No update, step counter untouched. */
+ * length scale's gradient is written to all d of its slots; slots of groups that do not train
+ * and padding slots are 0).  No update, step counter untouched. */
 int dgprf_potential_grad(const dgprf_plan_t *plan, const dgprf_chain_t *chain,
                          const dgprf_batch_t *batch, float data_size, int32_t full_bayes,
                          float *grad_out, void *stream);

@@ -231,3 +231,172 @@ def test_full_bayes_precond_rmsprop_masses(dev, golden):
     o = pl.lis_off[1]
     M_l1 = float(cpu(eng.hmass)[0, 9])
     assert rel_err(cpu(eng.hmom)[0, o:o + pl.d[1]], np.sqrt(M_l1) * h0[0, o:o + pl.d[1]]) < 1e-5
+
+
+# ----------------------------------------------------------------------------- engine level
+def load_chain(eng, p, c):
+    """Write oracle Params p into chain c of an Engine (z is shared by all chains)."""
+    pl = eng.layout
+    with torch.no_grad():
+        for l in range(eng.L):
+            eng.z_view(l).copy_(torch.as_tensor(p.z[l]))
+            eng.W_view(l, c).copy_(torch.as_tensor(p.W[l]))
+        h = eng.hyp_chain(c)
+        for l in range(eng.L):
+            h[l] = float(p.log_amp[l])
+            h[pl.lis_off[l]:pl.lis_off[l] + pl.d[l]] = torch.as_tensor(p.log_inv_ls[l])
+            h[pl.mean_off[l]:pl.mean_off[l] + pl.d[l]] = torch.as_tensor(p.mean[l])
+        h[eng.L] = float(p.lik_log_var)
+
+
+def random_params(rng, spec_args, ard):
+    d_in, d_out, kinds, n_rf, n_gp, cat, lik = spec_args
+    d = O.layer_widths(d_in, n_gp, cat)
+    L = len(kinds)
+    lis = [O.init_log_inv_ls(d[l]) + (0.2 * rng.standard_normal(d[l]) if ard[l] else 0.0)
+           for l in range(L)]
+    return O.Params(d_in, d_out, n_rf, n_gp, kinds, lik, cat, rng=rng,
+                    log_amp=[0.2 * rng.standard_normal() for _ in range(L)], log_inv_ls=lis,
+                    mean=[0.2 * rng.standard_normal(d[l]) for l in range(L)],
+                    lik_log_var=np.log(0.2) + 0.1 * rng.standard_normal())
+
+
+ENGINE_CASES = [
+    # d_in, d_out, kinds, n_rf, n_gp, cat, lik | ard | hyp flags
+    ((3, 1, ["RBF", "ARC", "RBF"], [32, 48, 20], [4, 5, 1], False, "gaussian"), [0, 1, 0],
+     ("kernel", "lik", "mean")),
+    ((5, 3, ["ARC", "RBF"], [40, 24], [6, 3], True, "softmax"), [1, 0], ("kernel",)),
+    ((2, 2, ["RBF", "RBF"], [16, 100], [3, 2], False, "gaussian"), [1, 1], ("mean", "lik")),
+    ((20, 1, ["RBF"], [64], [1], False, "gaussian"), [0], ("kernel", "lik")),
+]
+
+
+def engine_for(spec_args, ard, flags, C=1):
+    from dgprf import _native as N
+    from dgprf import engine as E
+    d_in, d_out, kinds, n_rf, n_gp, cat, lik = spec_args
+    hf = (N.HYP_KERNEL if "kernel" in flags else 0) | (N.HYP_LIK if "lik" in flags else 0) | \
+        (N.HYP_MEAN if "mean" in flags else 0)
+    spec = E.ModelSpec(d_in, d_out, [N.RBF if k == "RBF" else N.ARC for k in kinds], n_rf, n_gp,
+                       cat, N.LIK_GAUSSIAN if lik == "gaussian" else N.LIK_SOFTMAX, hf, ard)
+    return E.Engine(spec, n_chains=C, per_chain_hyp=True)
+
+
+def check_grad(eng, G, c, ref, tr):
+    pl = eng.layout
+    Gw = unpack(eng, G[:, :pl.w_total], chain=c)
+    Gh = hyper_of(eng, G[c, pl.w_total:])
+    for l in range(eng.L):
+        assert rel_err(Gw[l], ref["W"][l]) < 1e-4, ("W", l)
+        if tr.kernel:
+            assert group_err(Gh["log_inv_ls"][l], ref["log_inv_ls"][l]) < 5e-4, ("lis", l)
+        if tr.mean:
+            assert group_err(Gh["mean"][l], ref["mean"][l]) < 5e-4, ("mean", l)
+    if tr.kernel:
+        assert group_err([Gh["log_amp"][l] for l in range(eng.L)],
+                         [ref["log_amp"][l] for l in range(eng.L)]) < 5e-4
+    if ref["lik_log_var"] is not None:
+        assert abs(Gh["lik_log_var"] - ref["lik_log_var"]) < 5e-4 * (abs(ref["lik_log_var"]) + 1)
+    # slots of groups that do not train carry zero gradient
+    if not tr.kernel:
+        assert all(Gh["log_amp"][l] == 0 for l in range(eng.L))
+    if not tr.mean:
+        assert all(np.all(Gh["mean"][l] == 0) for l in range(eng.L))
+
+
+@pytest.mark.parametrize("case", range(len(ENGINE_CASES)))
+def test_full_bayes_engine_grad_flags_and_scalar_lengthscale(dev, case):
+    spec_args, ard, flags = ENGINE_CASES[case]
+    rng = np.random.default_rng(100 + case)
+    eng = engine_for(spec_args, ard, flags)
+    p = random_params(rng, spec_args, ard)
+    load_chain(eng, p, 0)
+    B, N_ = 77, 5000
+    X = rng.standard_normal((B, spec_args[0]))
+    Y = rng.standard_normal((B, spec_args[1])) if spec_args[6] == "gaussian" else \
+        rng.integers(0, spec_args[1], (B, 1)).astype(float)
+    tr = O.Trainable(kernel="kernel" in flags, lik="lik" in flags, mean="mean" in flags,
+                     ard=[bool(a) for a in ard])
+    G = eng.grad(X, Y, N_, full_bayes=True)
+    check_grad(eng, G, 0, O.grad_full(p, X, Y, N_, tr), tr)
+
+
+@pytest.mark.parametrize("case", [0, 1])
+def test_full_bayes_engine_step_scalar_lengthscale(dev, case):
+    """One step with injected noise; scalar length scales stay broadcast over their d slots."""
+    spec_args, ard, flags = ENGINE_CASES[case]
+    rng = np.random.default_rng(200 + case)
+    eng = engine_for(spec_args, ard, flags)
+    p = random_params(rng, spec_args, ard)
+    load_chain(eng, p, 0)
+    tr = O.Trainable(kernel="kernel" in flags, lik="lik" in flags, mean="mean" in flags,
+                     ard=[bool(a) for a in ard])
+    B, N_, lr, beta, T = 50, 2000, 0.01, 0.9, 1.0
+    X = rng.standard_normal((B, spec_args[0]))
+    Y = rng.standard_normal((B, spec_args[1])) if spec_args[6] == "gaussian" else \
+        rng.integers(0, spec_args[1], (B, 1)).astype(float)
+    keys = O.full_groups(p, tr)
+    shp = lambda k: np.shape(O.get_var(p, k, tr))
+    mom = {k: rng.standard_normal(shp(k)) for k in keys}
+    xi = {k: rng.standard_normal(shp(k)) for k in keys}
+    Mv = {k: (1.0 if k[0] == "W" else float(rng.uniform(0.5, 2.0))) for k in keys}
+    pl = eng.layout
+    slot = {"log_amp": lambda l: (l, l), "log_inv_ls": lambda l: (8 + l, pl.lis_off[l]),
+            "mean": lambda l: (16 + l, pl.mean_off[l]), "lik_log_var": lambda l: (24, eng.L)}
+    hm = torch.zeros(1, pl.hyp_total)
+    xh = torch.zeros(1, pl.hyp_total)
+    with torch.no_grad():
+        for k in keys:
+            nm, l = k
+            if nm == "W":
+                eng.mom_view(l).copy_(torch.as_tensor(mom[k]))
+                continue
+            s, o = slot[nm](l)
+            eng.hmass[0, s] = Mv[k]
+            n = int(np.size(mom[k]))
+            hm[0, o:o + n] = torch.as_tensor(np.reshape(mom[k], -1))
+            xh[0, o:o + n] = torch.as_tensor(np.reshape(xi[k], -1))
+        eng.hmom.copy_(hm)
+    eng.moments_ready = eng.hyper_moments_ready = True
+    xiw = pack(eng, [xi[("W", l)] for l in range(eng.L)])
+    eng.step(X, Y, N_, lr, beta, T, xi=xiw, full_bayes=True, xi_hyp=xh.to(dev))
+    new_m = O.sgmcmc_step_full(p, mom, X, Y, N_, lr, beta, T, Mv, xi, tr)
+    h = cpu(eng.hyp_chain(0))
+    hmv = cpu(eng.hmom[0])
+    for l in range(eng.L):
+        assert rel_err(cpu(eng.W_view(l)), p.W[l]) < 1e-5
+        assert close(h[pl.lis_off[l]:pl.lis_off[l] + pl.d[l]], p.log_inv_ls[l], 1e-5), l
+        assert close(h[pl.mean_off[l]:pl.mean_off[l] + pl.d[l]], p.mean[l], 1e-5), l
+        assert close(h[l], p.log_amp[l], 1e-5)
+        assert rel_err(cpu(eng.omega_view(l)), O.omega(p, l)) < 1e-5
+        if ("log_inv_ls", l) in new_m:
+            n = int(np.size(new_m[("log_inv_ls", l)]))
+            o = pl.lis_off[l]
+            assert group_err(hmv[o:o + n], new_m[("log_inv_ls", l)]) < 1e-4
+    if ("lik_log_var", None) in new_m:
+        assert close(h[eng.L], p.lik_log_var, 1e-5)
+
+
+def test_full_bayes_per_chain_hyper_parameters(dev):
+    """C chains, each with its own hyper-parameters / Omega (per_chain_hyp): every chain's
+    gradient and forward match the oracle at that chain's state."""
+    spec_args, ard, flags = ENGINE_CASES[0]
+    C = 3
+    rng = np.random.default_rng(300)
+    eng = engine_for(spec_args, ard, flags, C=C)
+    ps = [random_params(rng, spec_args, ard) for _ in range(C)]
+    for c in range(1, C):
+        ps[c].z = ps[0].z                       # z is shared by the chains
+    for c in range(C):
+        load_chain(eng, ps[c], c)
+    tr = O.Trainable(kernel=True, lik=True, mean=True, ard=[bool(a) for a in ard])
+    B, N_ = 64, 3000
+    X = rng.standard_normal((B, spec_args[0]))
+    Y = rng.standard_normal((B, 1))
+    G = eng.grad(X, Y, N_, full_bayes=True)
+    for c in range(C):
+        check_grad(eng, G, c, O.grad_full(ps[c], X, Y, N_, tr), tr)
+    # forward per chain uses that chain's Omega
+    F = eng.forward(X, f_out=True)["F"][0]
+    for c in range(C):
+        assert rel_err(cpu(F[c]), O.forward(ps[c], X)) < 2e-5, c
