@@ -98,6 +98,7 @@ def main():
     ap.add_argument("--steps-per-graph", type=int, default=100)
     ap.add_argument("--pred-samples", type=int, default=20)
     ap.add_argument("--multi-chains", type=int, default=64)
+    ap.add_argument("--full-bayes-steps", type=int, default=2000)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-reps", type=int, default=200)
@@ -241,6 +242,24 @@ def main():
                  "ms_per_step_all_chains": round(t_m * 1e3 / ((k_m // 50) * 50), 4)}
         del me, gph
 
+    # ---------------- full_bayesian=True steps (extra, not `value`): W + kernel / likelihood
+    # hyper-parameters sampled, Omega/c/sigma^2 rebuilt on the device every step
+    full_bayes = None
+    if args.full_bayes_steps > 0:
+        model.precond_update(None, N_, precond_type="identity", full_bayesian=True)
+        model.run_sgmcmc(X, Y, N_, args.steps_per_graph, full_bayesian=True, **run)
+        k_fb = max(args.steps_per_graph, args.full_bayes_steps // args.steps_per_graph *
+                   args.steps_per_graph)
+        barrier_sync()
+        t0 = time.perf_counter()
+        model.run_sgmcmc(X, Y, N_, k_fb, full_bayesian=True, **run)
+        barrier_sync()
+        t_fb = max_over_ranks(time.perf_counter() - t0)
+        assert torch.isfinite(model._engine.hyp).all(), "full-Bayes chain diverged"
+        full_bayes = {"steps_per_s": round(world * k_fb / t_fb, 2),
+                      "us_per_step": round(t_fb * 1e6 / k_fb, 3), "steps": k_fb,
+                      "sampled": "W, log_amplitude, log_inv_length_scale (ARD), lik_log_var"}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_seconds)
@@ -264,7 +283,7 @@ def main():
                            "test_loglik": round(ll, 6), "test_rmse": round(rmse, 6),
                            "ms_per_sample": round(t_pred * 1e3 / args.pred_samples, 4)},
             "roofline": roof, "roofline_predictive": roof_pred, "cpu_baseline": cpu,
-            "multi_chain": multi, "device": torch.cuda.get_device_name(dev),
+            "multi_chain": multi, "full_bayes": full_bayes, "device": torch.cuda.get_device_name(dev),
         }
         print(json.dumps(line), flush=True)
     if world > 1:

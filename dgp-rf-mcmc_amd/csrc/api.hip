@@ -115,7 +115,6 @@ hipError_t enqueue_step(const dgprf_plan_t& pl, const StepDev& sd, const UpdateD
   for (int l = pl.n_layers - 1; l >= 0 && e == hipSuccess; --l)
     e = dgprf::launch_step_bwd(pl, sd, l, s);
   if (e == hipSuccess) e = dgprf::launch_step_update(pl, sd, ud, nullptr, s, gather_next);
-  if (e == hipSuccess && sd.full_bayes) e = dgprf::launch_step_hyper(pl, sd, ud, s);
   return e;
 }
 
@@ -233,8 +232,8 @@ int dgprf_plan_init(dgprf_plan_t* pl) {
     pl->hpp_off[l] = ws;
     ws = align4(ws + (int64_t)pl->n_rt_pad * DGPRF_NS_MAX * align4(2 * pl->d[l] + 1));
   }
-  pl->hpl_off = ws;
-  ws = align4(ws + pl->n_rt_pad);
+  pl->hpl_off = ws;  // then DGPRF_MAX_LAYERS uint32 arrival counters of the hyper workgroups
+  ws = align4(ws + pl->n_rt_pad + DGPRF_MAX_LAYERS);
   pl->yb_cols = pl->likelihood == DGPRF_LIK_SOFTMAX ? 1 : pl->n_gp[L - 1];
   pl->xb_off = ws;
   ws = align4(ws + (int64_t)B * pl->d_in);

@@ -86,9 +86,9 @@ hipError_t launch_step_fwd(const dgprf_plan_t& pl, const StepDev& sd, int layer,
 hipError_t launch_step_bwd(const dgprf_plan_t& pl, const StepDev& sd, int layer, hipStream_t s);
 hipError_t launch_step_update(const dgprf_plan_t& pl, const StepDev& sd, const UpdateDev& ud,
                               const float* grad_in, hipStream_t s, bool gather_next = false);
-// full_bayesian=True: hyper-parameter gradients / updates and the Omega, c, sigma^2 rebuild
-hipError_t launch_step_hyper(const dgprf_plan_t& pl, const StepDev& sd, const UpdateDev& ud,
-                             hipStream_t s);
+// (sd.full_bayes: the same launch also runs the hyper-parameter workgroups — their gradients or
+// update and the Omega, c, sigma^2 rebuild)
+
 // minibatch rows of step *step + step_offset into the workspace (no-op for DGPRF_BATCH_DIRECT)
 hipError_t launch_gather(const dgprf_plan_t& pl, const StepDev& sd, hipStream_t s);
 hipError_t launch_advance(int64_t* step, int64_t by, hipStream_t s);

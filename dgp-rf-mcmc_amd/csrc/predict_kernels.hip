@@ -428,8 +428,8 @@ __host__ __device__ inline TileLds tile_lds(const dgprf_plan_t& pl, int notmax, 
 }
 
 // One layer for the calling wave's 16 rows.
-//   JW / JO: float4 W / Omega loads per thread per 64-feature block; KS: k-steps of A = Omega^T x
-//   (>= ceil(d/4); extra k-steps multiply staged zeros).
+//   JW / JO: float4 W / Omega loads per thread per 64-feature block (16 JO Omega rows staged);
+//   KS: k-steps of A = Omega^T x (ceil(d/4) <= KS <= 4 JO; extra k-steps multiply staged zeros).
 // Staged layouts: Omega [k][TW_OST] (x 1/2pi for the hardware sin/cos), W [h][feature][WST] with
 // WST = 16 NOT + 4 (g == 1: raw [h][64]); feature rows >= R are zeroed while staging, and output
 // columns o >= g are never stored, so the fragment reads need neither masks nor clamps and all
@@ -442,6 +442,9 @@ __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
                                            int lr, int lq, int64_t wrow0, int64_t n, float* fout) {
   constexpr int WST = tw_wst(NOT);
   constexpr bool REV = RBF && !DGPRF_PRECISE_TRIG_ON;
+  // the k-steps read Omega rows 0..4KS-1 of the staged block: all of them must be staged (rows >= d
+  // as zeros) — LDS is not cleared between kernels, and 0 * stale NaN is NaN
+  static_assert(4 * KS <= 16 * JO, "k-steps beyond the staged Omega rows");
   const int d = pl.d[layer], R = pl.n_rf[layer], g = pl.n_gp[layer];
   const int gp = layer > 0 ? pl.n_gp[layer - 1] : 0;
   const int tid = threadIdx.x;
@@ -659,7 +662,7 @@ void k_forward_tiles(
       tile_layer<NT, RB, G1_, JW, JO, 2, TPW>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, n, \
                                          fout);                                                     \
     else                                                                                            \
-      tile_layer<NT, RB, G1_, JW, JO, 8, TPW>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, n, \
+      tile_layer<NT, RB, G1_, JW, JO, 4 * JO, TPW>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, n, \
                                          fout);                                                     \
   } while (0)
     if (g == 1) {

@@ -26,6 +26,8 @@
 // fragment loads are unconditional with clamped addresses (no exec-masked branches or per-load
 // waits) and are issued before the dependent partial sums; minibatch rows of step t+1 are gathered
 // by step t's update kernel, so the forward never waits on the step counter or the permutation.
+#include <cstring>
+
 #include "dgprf_internal.h"
 
 namespace {
@@ -80,6 +82,25 @@ __device__ __forceinline__ bool tile_of_block(const LayerK& a, int& rt, int& sl)
   return rt < a.n_rt;
 }
 
+// full_bayesian=True hyper-parameter work, run by extra one-wave workgroups of k_step_update
+// (models/dgp.py:175-181, 199-216).  Layer l owns nb[l] workgroups starting at b0[l] (one each in
+// gradient-only mode); the last hyper workgroup handles the Gaussian lik_log_var.
+struct HypK {
+  float* hyp;          // chain 0 (chain stride hyp_cs)
+  float* hmom;         // [C][hyp_total]
+  const float* hmass;  // [C][DGPRF_HMASS]
+  const float* z;
+  float* omega;        // chain 0 (chain stride om_cs)
+  float* der;          // chain 0 (chain stride der_cs)
+  const float* ws;     // chain 0 workspace (chain stride ws_cs of UpdK)
+  int64_t hyp_cs, om_cs, der_cs, hyp_total, cnt_off;
+  int32_t n_blocks, flags, likelihood, pad;
+  int32_t d[DGPRF_MAX_LAYERS], R[DGPRF_MAX_LAYERS], kind[DGPRF_MAX_LAYERS], ard[DGPRF_MAX_LAYERS];
+  int32_t ns[DGPRF_MAX_LAYERS], nb[DGPRF_MAX_LAYERS], b0[DGPRF_MAX_LAYERS];
+  int64_t lis_off[DGPRF_MAX_LAYERS], mean_off[DGPRF_MAX_LAYERS], om_off[DGPRF_MAX_LAYERS];
+  int64_t hpp_off[DGPRF_MAX_LAYERS], hpl_off;
+};
+
 // Arguments of the update kernel (hot fields first: one burst of scalar loads).
 struct UpdK {
   float* theta;         // chain 0 (chain stride w_total)
@@ -101,6 +122,9 @@ struct UpdK {
   BatchDev bd;
   float* xb;
   float* yb;
+  // full_bayesian=True: the first hyp_blocks workgroups do the hyper-parameter work
+  int32_t hyp_blocks, pad_h;
+  HypK hk;
 };
 
 // v if ok else 0, written so that the compiler cannot sink the (always in-range, finite) load
@@ -451,6 +475,19 @@ __global__ __launch_bounds__(256) void k_step_bwd(const LayerK a) {
   // first chunk's fragments, issued before the dependent partial sums
   float omk[8];
   if (KS > 0) load_om_frag<KS>(om, R, d, chunk_f0(0), lr, lq, omk);
+  // full_bayesian=True: z fragments of the Dz = dA z^T tiles (d <= 32 when KS > 0: two 16-dim
+  // tiles prefetched with the Omega fragments; wider layers load them in the chunk loop)
+  constexpr int NZ = KS > 0 ? (4 * KS + 15) / 16 : 0;
+  const rsrc_t rz = make_rsrc(a.z, FB ? (int64_t)d * R : 0);
+  auto z_frag = [&](int f0, int dt) -> f4 {
+    const int k = dt * 16 + lr;
+    return bload4(rz, k < d && f0 + 4 * lq < R ? (uint32_t)(((int64_t)k * R + f0 + 4 * lq) * 4)
+                                               : DGPRF_OOB);
+  };
+  f4 zpf[NZ > 0 ? NZ : 1];
+  if (FB)
+#pragma unroll
+    for (int dt = 0; dt < NZ; ++dt) zpf[dt] = z_frag(chunk_f0(0), dt);
   // dPhi / dX A operands (W_l rows and Omega_l rows of this workgroup's 64-feature block) are
   // staged through LDS as W [2][64*g] (raw rows) and Omega [rows][OST]; the fragment reads zero
   // feature rows >= R.
@@ -619,6 +656,9 @@ __global__ __launch_bounds__(256) void k_step_bwd(const LayerK a) {
     if (f0 >= R) break;
     if (i > 0) {
       if (KS > 0) load_om_frag<KS>(om, R, d, f0, lr, lq, omk);
+      if (FB)
+#pragma unroll
+        for (int dt = 0; dt < NZ; ++dt) zpf[dt] = z_frag(f0, dt);
       if (dphi) {
         stage_load((sl * cpw + i) * 64);
         __syncthreads();  // every wave is done with the previous block
@@ -748,11 +788,16 @@ __global__ __launch_bounds__(256) void k_step_bwd(const LayerK a) {
       rs += __shfl_xor(rs, 32);
       // Dz = dA z^T in 16-dim tiles of the layer input (same contraction as dX with z rows),
       // contracted with the X tile over the 16 rows right away (linear in the features)
-      const rsrc_t rz = make_rsrc(a.z, (int64_t)d * R);
       for (int dt = 0; dt * 16 < d; ++dt) {
-        const int k = dt * 16 + lr;
-        const f4 zf = bload4(rz, k < d && f0 + 4 * lq < R
-                                     ? (uint32_t)(((int64_t)k * R + f0 + 4 * lq) * 4) : DGPRF_OOB);
+        f4 zf;
+        if (NZ > 0) {
+          zf = zpf[0];
+#pragma unroll
+          for (int q = 1; q < NZ; ++q)
+            if (dt == q) zf = zpf[q];
+        } else {
+          zf = z_frag(f0, dt);
+        }
         f4 dz = f4zero();
 #pragma unroll
         for (int r = 0; r < 4; ++r) dz = mfma16(zf[r], da[r], dz);
@@ -880,20 +925,310 @@ __device__ __forceinline__ f2 bload2(rsrc_t r, uint32_t byte_off) {
   return __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(r, byte_off, 0, 0));
 }
 
+// Schedule of step t (utils.py:49-73 via experiments/utils_training.py:41-61 when CYC).
+template <bool CYC>
+__device__ __forceinline__ void step_schedule(const UpdateDev& ud, int64_t t, float* lr, float* T,
+                                              int* resample) {
+  *lr = ud.lr;
+  *T = ud.temperature;
+  *resample = ud.resample;
+  if (CYC) {
+    if (t < ud.start_step) {  // burn-in: fixed lr, zero temperature
+      *T = 0.f;
+      *resample = 0;
+    } else {
+      const int64_t si = t - ud.start_step + 1;
+      const float rate = cyclical_rate(si, ud.cycle_length);
+      *lr = ud.lr * (rate * rate);
+      *T = 1.f;
+      *resample = ud.resample_head && (si % ud.cycle_length == 1);
+    }
+  }
+}
+
+// One N(0,1) of the hyper-parameter streams (not inlined: the hyper path runs once per step on
+// a few CUs, where instruction-cache misses, not arithmetic, set its duration).
+__device__ __noinline__ float normal_at(uint64_t seed, uint64_t t, uint32_t purpose, uint32_t chain,
+                                        int64_t slot) {
+  const f4 z = philox_normal4(seed, t, purpose, chain, (uint32_t)(slot >> 2));
+  return z[slot & 3];
+}
+
+// Omega elements rebuilt per hyper workgroup (16 per lane)
+constexpr int HYP_EPB = UPD_THREADS * 16;
+
+// One hyper workgroup (full_bayesian=True).  The backward left per-workgroup partials
+//   [n_rt][NSM][hs]: sum_b X[b][k](dA z^T)[b][k] (k < d), sum_b X[b][k] rowsum(dA)[b], sum dPhi*Phi
+// and per row tile the Gaussian lik_log_var term.  Every workgroup of layer l reduces them in the
+// same fixed order, forms
+//   g_log_amp = sum dPhi*Phi + log_amp/N,   g_lis[k] = exp(lis[k]) sum(...)[k] + lis[k]/N
+//   (scalar lis: summed over k),            g_mean[k] = sum_b X[b][k] rowsum(dA)[b] + mean[k]/N
+// and applies the SGHMC update of models/dgp.py:206-216 (own momentum, mass and Philox stream) to
+// identical new values in LDS; it then rebuilds its HYP_EPB elements of
+// Omega_l = exp(lis)[:,None] z_l + mean[:,None] (kernels/RBF.py:43-53, layers/rf_layers.py:34-38).
+// The last workgroup of the layer to finish reading the old values (arrival counter, no waiting)
+// stores the new hyp / hmom, so no workgroup can read a half-updated set.  Gradient-only mode
+// writes dU/d(hyper) into grad_out instead (one workgroup per layer, nothing rebuilt).
+template <bool GONLY, bool XI, bool CYC>
+__device__ void hyper_block(const UpdK& a, int hb, int chain, float* sm, int sb) {
+  const HypK& k = a.hk;
+  const int tid = threadIdx.x, L = a.n_layers;
+  constexpr int NT = UPD_THREADS;
+  float* hyp = k.hyp + (int64_t)chain * k.hyp_cs;
+  float* hm = k.hmom + (int64_t)chain * k.hyp_total;
+  const float* hmass = k.hmass + chain * DGPRF_HMASS;
+  float* gout = a.grad_out + (int64_t)chain * a.grad_cs + a.w_total;
+  const UpdateDev& ud = a.ud;
+  const float N = ud.data_size;
+  const int64_t t = *a.step + (int64_t)a.step_offset;
+  float lr, T;
+  int resample;
+  step_schedule<CYC>(ud, t, &lr, &T, &resample);
+  const float h = sqrtf(lr / N), beta = ud.beta;
+  // SGHMC update of hyper slot `slot` (value v, momentum m, mass slot midx); returns the new value
+  auto upd = [&](int64_t slot, float g, float v, float m, int midx, float* m_out) -> float {
+    if (GONLY) {
+      gout[slot] = g;
+      return v;
+    }
+    const float M = hmass[midx];
+    if (resample)
+      m = (XI && ud.xi_hyp_resample)
+              ? ud.xi_hyp_resample[(int64_t)chain * k.hyp_total + slot]
+              : normal_at(a.seed, (uint64_t)t, DGPRF_RNG_HYPER_RESAMPLE, chain, slot);
+    const float eps = (XI && ud.xi_hyp) ? ud.xi_hyp[(int64_t)chain * k.hyp_total + slot]
+                                        : normal_at(a.seed, (uint64_t)t, DGPRF_RNG_HYPER, chain, slot);
+    const float mn = beta * m - (h * N) * g + sqrtf(2.0f * (1.0f - beta) * T * M) * eps;
+    *m_out = mn;
+    return v + (h * (1.0f / M)) * mn;
+  };
+  if (hb == k.n_blocks - 1) {  // Gaussian lik_log_var (likelihoods/gaussian.py:12)
+    const bool lik_tr = (k.flags & DGPRF_HYP_LIK) && k.likelihood == DGPRF_LIK_GAUSSIAN;
+    if (GONLY) {  // slots no workgroup owns (padding, groups that do not train) read as 0
+      for (int64_t s = tid; s < k.hyp_total; s += NT) {
+        bool owned = s < L ? (k.flags & DGPRF_HYP_KERNEL) != 0 : (s == L && lik_tr);
+        for (int q = 0; q < L; ++q) {
+          owned |= (k.flags & DGPRF_HYP_KERNEL) && s >= k.lis_off[q] && s < k.lis_off[q] + k.d[q];
+          owned |= (k.flags & DGPRF_HYP_MEAN) && s >= k.mean_off[q] && s < k.mean_off[q] + k.d[q];
+        }
+        if (!owned) gout[s] = 0.f;
+      }
+    }
+    if (lik_tr && tid == 0) {
+      const float* hpl = k.ws + (int64_t)chain * a.ws_cs + k.hpl_off;
+      float s = 0.f;
+      for (int rt = 0; rt < a.n_rt; ++rt) s += hpl[rt];
+      const float v0 = hyp[L];
+      float mn = 0.f;
+      const float v = upd(L, s + v0 / N, v0, GONLY ? 0.f : hm[L], 24, &mn);
+      if (!GONLY) {
+        hm[L] = mn;
+        hyp[L] = v;
+        k.der[(int64_t)chain * k.der_cs + DGPRF_MAX_LAYERS] = expf(v);
+      }
+    }
+    return;
+  }
+  int l = 0;
+  for (int q = 1; q < L; ++q)
+    if (hb >= k.b0[q]) l = q;
+  const int j = hb - k.b0[l], d = k.d[l], R = k.R[l], nv = 2 * d + 1, hs = (nv + 3) & ~3;
+  const int Q = hs >> 2, ns = k.ns[l], P = a.n_rt * ns, RG = Q >= NT ? 1 : NT / Q;
+  const bool kern = (k.flags & DGPRF_HYP_KERNEL) != 0, mean = (k.flags & DGPRF_HYP_MEAN) != 0;
+  const int64_t lis = k.lis_off[l], mo = k.mean_off[l];
+  // LDS: totals | old values | old momenta | new values | exp(new lis) | row-group partials | tree
+  float* tot = sm;
+  float* ov = tot + hs;   // [0] log_amp, [1+k] log_inv_ls, [1+d+k] mean
+  float* om = ov + hs;
+  float* nvv = om + hs;
+  float* els = nvv + hs;  // exp(new lis)[d]
+  float* part = els + hs;                       // [RG][hs]
+  float* red = part + (4 * NT > hs ? 4 * NT : hs);  // [NT] tree, [NT] last-arrival flag
+  auto slot_of = [&](int e) -> int64_t { return e == 0 ? (int64_t)l : (e <= d ? lis + e - 1 : mo + e - 1 - d); };
+  // (0) z of this workgroup's Omega slice and the old values / momenta first: independent loads
+  float* omg = k.omega + (int64_t)chain * k.om_cs + k.om_off[l];
+  const int64_t n_el = (int64_t)d * R, base = (int64_t)j * HYP_EPB;
+  f4 zv[4];
+  if (!GONLY) {
+    const rsrc_t rz = make_rsrc(k.z + k.om_off[l], n_el);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t i = base + 4 * (tid + NT * u);
+      zv[u] = bload4(rz, i < n_el ? (uint32_t)(i * 4) : DGPRF_OOB);
+    }
+  }
+  for (int e = tid; e < 1 + 2 * d; e += NT) {
+    const int64_t s = slot_of(e);
+    ov[e] = hyp[s];
+    om[e] = GONLY ? 0.f : hm[s];
+  }
+  __syncthreads();  // every old value of this workgroup has been read
+  DGPRF_STAMP(sb, 1);
+  // arrival on the layer's counter (its return overlaps the partial loads below)
+  unsigned* cnt = reinterpret_cast<unsigned*>(const_cast<float*>(k.ws) + (int64_t)chain * a.ws_cs +
+                                              k.cnt_off) + l;
+  unsigned arrived = 0u;
+  if (!GONLY && k.nb[l] > 1 && tid == 0) arrived = atomicAdd(cnt, 1u);
+  // (1) partial row sums: up to HYP_U loads per lane in flight, summed in row order
+  // rows p = rt * ns + sl of a row group advance by RG: (rt, sl) tracked without divisions
+  constexpr int HYP_U = 8;
+  const float* hp = k.ws + (int64_t)chain * a.ws_cs + k.hpp_off[l];
+  const rsrc_t rh = make_rsrc(hp, (int64_t)a.n_rt * NSM * hs);
+  const int st_rt = RG / ns, st_sl = RG - st_rt * ns;
+  for (int i = tid; i < RG * Q; i += NT) {
+    const int q = i % Q, rg = i / Q;
+    int rt = rg / ns, sl = rg - rt * ns;
+    f4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int p0 = rg; p0 < P; p0 += HYP_U * RG) {
+      f4 v[HYP_U];
+#pragma unroll
+      for (int u = 0; u < HYP_U; ++u) {
+        v[u] = bload4(rh, rt < a.n_rt ? (uint32_t)(((rt * NSM + sl) * hs + 4 * q) * 4) : DGPRF_OOB);
+        rt += st_rt;
+        sl += st_sl;
+        if (sl >= ns) {
+          sl -= ns;
+          ++rt;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < HYP_U; ++u) acc += v[u];
+    }
+    *reinterpret_cast<f4*>(part + rg * hs + 4 * q) = acc;
+  }
+  DGPRF_STAMP(sb, 2);
+  __syncthreads();
+  for (int e = tid; e < nv; e += NT) {
+    float s = 0.f;
+    for (int rg = 0; rg < RG; ++rg) s += part[rg * hs + e];
+    tot[e] = s;
+  }
+  __syncthreads();
+  DGPRF_STAMP(sb, 3);
+  // (2) new values: one update site for every slot (scalar lis: one slot, broadcast after)
+  const bool scalar_lis = kern && !k.ard[l];
+  float gsc = 0.f;
+  if (scalar_lis) {  // one length scale: its gradient sums over the d dims (fixed-order tree)
+    float sp = 0.f;
+    for (int kk = tid; kk < d; kk += NT) sp += expf(ov[1 + kk]) * tot[kk];
+    red[tid] = sp;
+    __syncthreads();
+    for (int w = NT / 2; w > 0; w >>= 1) {
+      if (tid < w) red[tid] += red[tid + w];
+      __syncthreads();
+    }
+    gsc = red[0];
+  }
+  for (int e = tid; e < 1 + 2 * d; e += NT) {
+    float v = ov[e], mn = om[e];
+    bool tr;
+    float g;
+    int midx;
+    int64_t slot;
+    if (e == 0) {
+      tr = kern;
+      g = tot[2 * d];
+      midx = l;
+      slot = l;
+    } else if (e <= d) {
+      tr = kern && (!scalar_lis || e == 1);
+      g = scalar_lis ? gsc : expf(ov[e]) * tot[e - 1];
+      midx = 8 + l;
+      slot = lis + e - 1;
+    } else {
+      tr = mean;
+      g = tot[e - 1];
+      midx = 16 + l;
+      slot = mo + e - 1 - d;
+    }
+    if (tr) v = upd(slot, g + ov[e] / N, ov[e], om[e], midx, &mn);
+    nvv[e] = v;
+    om[e] = mn;
+  }
+  if (scalar_lis) {
+    __syncthreads();
+    for (int kk = 1 + tid; kk < d; kk += NT) {
+      nvv[1 + kk] = nvv[1];
+      om[1 + kk] = om[1];
+      if (GONLY) gout[lis + kk] = gsc + ov[1] / N;
+    }
+  }
+  if (GONLY) return;
+  __syncthreads();
+  DGPRF_STAMP(sb, 4);
+  for (int kk = tid; kk < d; kk += NT) els[kk] = expf(nvv[1 + kk]);
+  // (3) the last workgroup of the layer to arrive stores the new hyp / hmom
+  bool last = k.nb[l] == 1;
+  if (!last) {
+    if (tid == 0) {
+      const bool lst = arrived == (unsigned)k.nb[l] - 1u;
+      if (lst) *cnt = 0u;
+      red[NT] = lst ? 1.f : 0.f;
+    }
+    __syncthreads();
+    last = red[NT] != 0.f;
+  } else {
+    __syncthreads();
+  }
+  if (last) {
+    for (int e = tid; e < 1 + 2 * d; e += NT) {
+      const bool tr = e == 0 ? kern : (e <= d ? kern : mean);
+      if (!tr) continue;
+      const int64_t s = slot_of(e);
+      hyp[s] = nvv[e];
+      hm[s] = om[e];
+    }
+  }
+  DGPRF_STAMP(sb, 5);
+  // (4) this workgroup's slice of Omega_l and c_l (layers/rf_layers.py:44,90)
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int64_t i = base + 4 * (tid + NT * u);
+    if (i >= n_el) continue;
+    f4 o;
+    int kk = (int)((uint32_t)i / (uint32_t)R), rc = (int)i - kk * R;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int kc = kk < d ? kk : d - 1;
+      o[c] = els[kc] * zv[u][c] + nvv[1 + d + kc];
+      for (++rc; rc >= R; rc -= R) ++kk;
+    }
+    if (i + 3 < n_el) {
+      *reinterpret_cast<f4*>(omg + i) = o;
+    } else {
+      for (int c = 0; c < 4 && i + c < n_el; ++c) omg[i + c] = o[c];
+    }
+  }
+  if (j == 0 && tid == 0) {
+    const float amp = expf(nvv[0]), sq = sqrtf((float)R);
+    k.der[(int64_t)chain * k.der_cs + l] = k.kind[l] == DGPRF_RBF ? amp / sq : (sqrtf(2.f) * amp) / sq;
+  }
+#ifdef DGPRF_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  DGPRF_STAMP(sb, 14);
+}
+
 template <bool GIN, bool GONLY, bool XI, bool CYC>
 __global__ __launch_bounds__(UPD_THREADS) void k_step_update(const UpdK a) {
+  extern __shared__ __attribute__((aligned(16))) float usm[];
   const int chain = blockIdx.y;
   const int stamp_base = 16 * 4096 + blockIdx.y * gridDim.x + blockIdx.x;
   DGPRF_STAMP(stamp_base, 0);
-  if ((int)blockIdx.x >= a.upd_blocks) {  // dedicated blocks: rows of step t+1 (off the path)
+  if (!GIN && (int)blockIdx.x < a.hyp_blocks) {  // full_bayesian=True hyper-parameters
+    hyper_block<GONLY, XI, CYC>(a, (int)blockIdx.x, chain, usm, stamp_base);
+    return;
+  }
+  const int bx = (int)blockIdx.x - a.hyp_blocks;
+  if (bx >= a.upd_blocks) {  // dedicated blocks: rows of step t+1 (off the path)
     const int64_t t = *a.step + (int64_t)a.step_offset;
-    const int b = ((int)blockIdx.x - a.upd_blocks) * UPD_THREADS + threadIdx.x;
+    const int b = (bx - a.upd_blocks) * UPD_THREADS + threadIdx.x;
     if (a.gather_next && b < a.B)
       gather_row(a.bd, a.B, a.d_in, a.yb_cols, a.xb + (int64_t)chain * a.ws_cs,
                  a.yb + (int64_t)chain * a.ws_cs, chain, t + 1, b);
     return;
   }
-  const int e0 = 2 * ((int)blockIdx.x * UPD_THREADS + (int)threadIdx.x);
+  const int e0 = 2 * (bx * UPD_THREADS + (int)threadIdx.x);
   const uint32_t off = (uint32_t)e0 * 4u;
   const int64_t cw = (int64_t)chain * a.w_total;
   const rsrc_t rth = make_rsrc(a.theta + cw, a.w_total);
@@ -932,20 +1267,9 @@ __global__ __launch_bounds__(UPD_THREADS) void k_step_update(const UpdK a) {
   // the step counter (written by the previous step's k_advance) is read only now, after the
   // parameter and partial loads are in flight
   const int64_t t = *a.step + (int64_t)a.step_offset;
-  float lr = ud.lr, T = ud.temperature;
-  int resample = ud.resample;
-  if (CYC) {
-    if (t < ud.start_step) {  // burn-in: fixed lr, zero temperature
-      T = 0.f;
-      resample = 0;
-    } else {
-      const int64_t si = t - ud.start_step + 1;
-      const float rate = cyclical_rate(si, ud.cycle_length);
-      lr = ud.lr * (rate * rate);
-      T = 1.f;
-      resample = ud.resample_head && (si % ud.cycle_length == 1);
-    }
-  }
+  float lr, T;
+  int resample;
+  step_schedule<CYC>(ud, t, &lr, &T, &resample);
   const float h = sqrtf(lr / N);
   const float beta = ud.beta;
   const uint32_t quad = (uint32_t)(e0 >> 2);
@@ -979,201 +1303,6 @@ __global__ __launch_bounds__(UPD_THREADS) void k_step_update(const UpdK a) {
   DGPRF_STAMP(stamp_base, 14);
 }
 
-// ------------------------------------------------------------------------- hyper-parameters
-// full_bayesian=True (models/dgp.py:175-181, 199-216): one workgroup per layer (+ one for the
-// Gaussian lik_log_var) reduces the backward's per-workgroup partials in a fixed order, forms
-//   g_log_amp   = sum dPhi*Phi                          + log_amp/N
-//   g_lis[k]    = exp(lis[k]) sum_b X[b][k](dA z^T)[b][k] + lis[k]/N   (scalar lis: summed over k)
-//   g_mean[k]   = sum_b X[b][k] rowsum(dA)[b]           + mean[k]/N
-//   g_lik       = sum_b sum_o (1 - (y-F)^2/var)/(2B)    + lik_log_var/N
-// applies the same SGHMC update as W (own momentum, mass and Philox stream) and rebuilds the
-// layer's Omega / c (and sigma^2), so the next step sees the new hyper-parameters.
-struct HypK {
-  float* hyp;  // chain 0 (chain stride hyp_cs)
-  float* hmom;  // [C][hyp_total]
-  const float* hmass;
-  const float* z;
-  float* omega;
-  float* der;
-  const float* ws;
-  const int64_t* step;
-  float* grad_out;
-  uint64_t seed;
-  int64_t ws_cs, hyp_cs, om_cs, der_cs, hyp_total, grad_cs, w_total;
-  int32_t n_layers, n_rt, step_offset, flags, likelihood, vt;
-  int32_t d[DGPRF_MAX_LAYERS], R[DGPRF_MAX_LAYERS], kind[DGPRF_MAX_LAYERS], ard[DGPRF_MAX_LAYERS];
-  int32_t ns[DGPRF_MAX_LAYERS];
-  int64_t lis_off[DGPRF_MAX_LAYERS], mean_off[DGPRF_MAX_LAYERS], om_off[DGPRF_MAX_LAYERS];
-  int64_t hpp_off[DGPRF_MAX_LAYERS], hpl_off;
-  UpdateDev ud;
-};
-
-__device__ __forceinline__ float normal_at(uint64_t seed, uint64_t t, uint32_t purpose,
-                                           uint32_t chain, int64_t slot) {
-  const f4 z = philox_normal4(seed, t, purpose, chain, (uint32_t)(slot >> 2));
-  return z[slot & 3];
-}
-
-template <bool GONLY, bool XI, bool CYC>
-__global__ __launch_bounds__(256) void k_step_hyper(const HypK a) {
-  extern __shared__ __attribute__((aligned(16))) float hsm[];
-  const int chain = blockIdx.y, blk = blockIdx.x, L = a.n_layers, tid = threadIdx.x;
-  float* hyp = a.hyp + (int64_t)chain * a.hyp_cs;
-  float* hm = a.hmom + (int64_t)chain * a.hyp_total;
-  const UpdateDev& ud = a.ud;
-  const float N = ud.data_size;
-  const int64_t t = *a.step + (int64_t)a.step_offset;
-  float lr = ud.lr, T = ud.temperature;
-  int resample = ud.resample;
-  if (CYC) {
-    if (t < ud.start_step) {
-      T = 0.f;
-      resample = 0;
-    } else {
-      const int64_t si = t - ud.start_step + 1;
-      const float rate = cyclical_rate(si, ud.cycle_length);
-      lr = ud.lr * (rate * rate);
-      T = 1.f;
-      resample = ud.resample_head && (si % ud.cycle_length == 1);
-    }
-  }
-  const float h = sqrtf(lr / N), beta = ud.beta;
-  // SGHMC update of hyper slot `slot` with gradient g (models/dgp.py:206-216); returns the value
-  auto upd = [&](int64_t slot, float g, int midx, float* mom_out) -> float {
-    if (GONLY) {
-      a.grad_out[(int64_t)chain * a.grad_cs + a.w_total + slot] = g;
-      return hyp[slot];
-    }
-    const float M = a.hmass[chain * DGPRF_HMASS + midx];
-    float m = hm[slot];
-    if (resample)
-      m = (XI && ud.xi_hyp_resample)
-              ? ud.xi_hyp_resample[(int64_t)chain * a.hyp_total + slot]
-              : normal_at(a.seed, (uint64_t)t, DGPRF_RNG_HYPER_RESAMPLE, chain, slot);
-    const float eps = (XI && ud.xi_hyp) ? ud.xi_hyp[(int64_t)chain * a.hyp_total + slot]
-                                        : normal_at(a.seed, (uint64_t)t, DGPRF_RNG_HYPER, chain, slot);
-    const float mn = beta * m - (h * N) * g + sqrtf(2.0f * (1.0f - beta) * T * M) * eps;
-    *mom_out = mn;
-    return hyp[slot] + (h * (1.0f / M)) * mn;
-  };
-  if (blk == L) {  // Gaussian lik_log_var
-    const bool lik_tr = (a.flags & DGPRF_HYP_LIK) && a.likelihood == DGPRF_LIK_GAUSSIAN;
-    if (GONLY) {  // slots no block owns (padding, groups that do not train) read as 0
-      for (int64_t s = tid; s < a.hyp_total; s += 256) {
-        bool owned = s < L ? (a.flags & DGPRF_HYP_KERNEL) != 0 : (s == L && lik_tr);
-        for (int q = 0; q < L; ++q) {
-          owned |= (a.flags & DGPRF_HYP_KERNEL) && s >= a.lis_off[q] && s < a.lis_off[q] + a.d[q];
-          owned |= (a.flags & DGPRF_HYP_MEAN) && s >= a.mean_off[q] && s < a.mean_off[q] + a.d[q];
-        }
-        if (!owned) a.grad_out[(int64_t)chain * a.grad_cs + a.w_total + s] = 0.f;
-      }
-    }
-    if (lik_tr && tid == 0) {
-      const float* hpl = a.ws + (int64_t)chain * a.ws_cs + a.hpl_off;
-      float s = 0.f;
-      for (int rt = 0; rt < a.n_rt; ++rt) s += hpl[rt];
-      float mn = 0.f;
-      const float v = upd(L, s + hyp[L] / N, 24, &mn);
-      if (!GONLY) {
-        hm[L] = mn;
-        hyp[L] = v;
-        a.der[(int64_t)chain * a.der_cs + DGPRF_MAX_LAYERS] = expf(v);
-      }
-    }
-    return;
-  }
-  const int l = blk, d = a.d[l], R = a.R[l], nv = 2 * d + 1, hs = (nv + 3) & ~3;
-  const int ns = a.ns[l], P = a.n_rt * ns, vt = a.vt;
-  float* stage = hsm;                   // [P][vt]
-  float* tot = hsm + P * vt;            // [hs]
-  float* red = tot + hs;                // [256]
-  const float* hp = a.ws + (int64_t)chain * a.ws_cs + a.hpp_off[l];
-  const rsrc_t rh = make_rsrc(hp, (int64_t)a.n_rt * NSM * hs);
-  // fixed-order sums over (row tile, slice) of every value, vt values at a time through LDS
-  for (int e0 = 0; e0 < nv; e0 += vt) {
-    const int q4 = vt >> 2;
-    for (int i = tid; i < P * q4; i += 256) {
-      const int row = i / q4, q = i - row * q4, rt = row / ns, sl = row - rt * ns;
-      const int e = e0 + 4 * q;
-      const f4 v = bload4(rh, e < hs ? (uint32_t)((((int64_t)rt * NSM + sl) * hs + e) * 4) : DGPRF_OOB);
-      *reinterpret_cast<f4*>(stage + row * vt + 4 * q) = v;
-    }
-    __syncthreads();
-    for (int e = tid; e < vt && e0 + e < nv; e += 256) {
-      float acc = 0.f;
-      for (int row = 0; row < P; ++row) acc += stage[row * vt + e];
-      tot[e0 + e] = acc;
-    }
-    __syncthreads();
-  }
-  const int64_t lis = a.lis_off[l], mo = a.mean_off[l];
-  if (a.flags & DGPRF_HYP_KERNEL) {
-    if (tid == 0) {
-      float mn = 0.f;
-      const float v = upd(l, tot[2 * d] + hyp[l] / N, l, &mn);
-      if (!GONLY) {
-        hm[l] = mn;
-        hyp[l] = v;
-      }
-    }
-    if (a.ard[l]) {
-      for (int k = tid; k < d; k += 256) {
-        const float lk = hyp[lis + k];
-        float mn = 0.f;
-        const float v = upd(lis + k, expf(lk) * tot[k] + lk / N, 8 + l, &mn);
-        if (!GONLY) {
-          hm[lis + k] = mn;
-          hyp[lis + k] = v;
-        }
-      }
-    } else {  // one scalar length scale: its gradient sums over the d dims
-      float part = 0.f;
-      for (int k = tid; k < d; k += 256) part += expf(hyp[lis + k]) * tot[k];
-      red[tid] = part;
-      __syncthreads();
-      for (int w = 128; w > 0; w >>= 1) {
-        if (tid < w) red[tid] += red[tid + w];
-        __syncthreads();
-      }
-      if (tid == 0) {
-        float mn = 0.f;
-        const float v = upd(lis, red[0] + hyp[lis] / N, 8 + l, &mn);
-        if (GONLY) {
-          for (int k = 1; k < d; ++k) a.grad_out[(int64_t)chain * a.grad_cs + a.w_total + lis + k] =
-              a.grad_out[(int64_t)chain * a.grad_cs + a.w_total + lis];
-        } else {
-          for (int k = 0; k < d; ++k) {
-            hm[lis + k] = mn;
-            hyp[lis + k] = v;
-          }
-        }
-      }
-    }
-  }
-  if (a.flags & DGPRF_HYP_MEAN) {
-    for (int k = tid; k < d; k += 256) {
-      float mn = 0.f;
-      const float v = upd(mo + k, tot[d + k] + hyp[mo + k] / N, 16 + l, &mn);
-      if (!GONLY) {
-        hm[mo + k] = mn;
-        hyp[mo + k] = v;
-      }
-    }
-  }
-  if (GONLY) return;
-  __syncthreads();  // this layer's new hyper-parameters are in place
-  // Omega_l = exp(lis)[:,None] z_l + mean[:,None], c_l (kernels/RBF.py:43-53, rf_layers.py:34-44)
-  float* om = a.omega + (int64_t)chain * a.om_cs + a.om_off[l];
-  const float* zl = a.z + a.om_off[l];
-  for (int64_t i = tid; i < (int64_t)d * R; i += 256) {
-    const int k = (int)(i / R);
-    om[i] = expf(hyp[lis + k]) * zl[i] + hyp[mo + k];
-  }
-  if (tid == 0) {
-    const float amp = expf(hyp[l]), sq = sqrtf((float)R);
-    a.der[(int64_t)chain * a.der_cs + l] = a.kind[l] == DGPRF_RBF ? amp / sq : (sqrtf(2.f) * amp) / sq;
-  }
-}
 
 __global__ void k_advance(int64_t* step, int64_t by) {
   if (threadIdx.x == 0 && blockIdx.x == 0) *step += by;
@@ -1376,17 +1505,69 @@ hipError_t launch_step_update(const dgprf_plan_t& pl, const StepDev& sd, const U
   a.yb = sd.ws ? sd.ws + pl.yb_off : nullptr;
   const int64_t pairs = pl.w_total / 2;
   a.upd_blocks = (int)((pairs + UPD_THREADS - 1) / UPD_THREADS);
-  const int64_t blocks =
-      a.upd_blocks + (a.gather_next ? (pl.batch + UPD_THREADS - 1) / UPD_THREADS : 0);
-  dim3 grid((unsigned)blocks, pl.n_chains);
   const bool gin = grad_in != nullptr, gonly = ud.grad_only != 0;
-  const bool xi = ud.xi != nullptr || ud.xi_resample != nullptr;
+  const bool fb = sd.full_bayes && !gin;
+  // full_bayesian=True: hyper workgroups first (per layer ceil(d R / HYP_EPB) for the Omega
+  // rebuild, one in gradient-only mode), then the lik_log_var workgroup
+  a.hyp_blocks = 0;
+  a.pad_h = 0;
+  std::memset(&a.hk, 0, sizeof(a.hk));
+  size_t lds = 0;
+  if (fb) {
+    HypK& k = a.hk;
+    k.hyp = sd.hyp;
+    k.hmom = sd.hmom;
+    k.hmass = sd.hmass;
+    k.z = sd.z;
+    k.omega = sd.omega;
+    k.der = sd.der;
+    k.ws = sd.ws;
+    k.hyp_cs = sd.hyp_cs;
+    k.om_cs = sd.om_cs;
+    k.der_cs = sd.der_cs;
+    k.hyp_total = pl.hyp_total;
+    k.cnt_off = pl.hpl_off + pl.n_rt_pad;
+    k.flags = pl.hyp_flags;
+    k.likelihood = pl.likelihood;
+    int nb_total = 0, hsmax = 4;
+    for (int l = 0; l < pl.n_layers; ++l) {
+      const int64_t n_el = (int64_t)pl.d[l] * pl.n_rf[l];
+      const int nb = gonly ? 1 : (int)((n_el + HYP_EPB - 1) / HYP_EPB);
+      k.d[l] = pl.d[l];
+      k.R[l] = pl.n_rf[l];
+      k.kind[l] = pl.kind[l];
+      k.ard[l] = pl.ard[l];
+      k.ns[l] = pl.ns[l];
+      k.nb[l] = nb < 1 ? 1 : nb;
+      k.b0[l] = nb_total;
+      nb_total += k.nb[l];
+      k.lis_off[l] = pl.lis_off[l];
+      k.mean_off[l] = pl.mean_off[l];
+      k.om_off[l] = pl.omega_off[l];
+      k.hpp_off[l] = pl.hpp_off[l];
+      hsmax = max(hsmax, round4(2 * pl.d[l] + 1));
+      if (n_el >= (int64_t)1 << 29 || (int64_t)pl.n_rt_pad * NSM * round4(2 * pl.d[l] + 1) >= (int64_t)1 << 29)
+        return hipErrorInvalidValue;  // 32-bit buffer offsets
+    }
+    k.hpl_off = pl.hpl_off;
+    k.n_blocks = nb_total + 1;
+    a.hyp_blocks = k.n_blocks;
+    lds = (size_t)(5 * hsmax + max(4 * UPD_THREADS, hsmax) + UPD_THREADS + 4) * sizeof(float);
+  }
+  const int64_t blocks = a.hyp_blocks + a.upd_blocks +
+                         (a.gather_next ? (pl.batch + UPD_THREADS - 1) / UPD_THREADS : 0);
+  dim3 grid((unsigned)blocks, pl.n_chains);
+  const bool xi = ud.xi != nullptr || ud.xi_resample != nullptr ||
+                  (fb && (ud.xi_hyp != nullptr || ud.xi_hyp_resample != nullptr));
   const bool cyc = ud.schedule == DGPRF_SCHED_CYCLICAL;
   const int sel = (gin ? 8 : 0) | (gonly ? 4 : 0) | (xi ? 2 : 0) | (cyc ? 1 : 0);
 #define DGPRF_UPD_CASE(S)                                                                     \
   case S:                                                                                    \
+    if (lds > 65536)                                                                         \
+      dgprf::set_lds_limit(                                                                  \
+          (const void*)k_step_update<(S & 8) != 0, (S & 4) != 0, (S & 2) != 0, (S & 1) != 0>, lds); \
     hipLaunchKernelGGL((k_step_update<(S & 8) != 0, (S & 4) != 0, (S & 2) != 0, (S & 1) != 0>), \
-                       grid, dim3(UPD_THREADS), 0, s, a);                                    \
+                       grid, dim3(UPD_THREADS), lds, s, a);                                  \
     break;
   switch (sel) {
     DGPRF_UPD_CASE(0) DGPRF_UPD_CASE(1) DGPRF_UPD_CASE(2) DGPRF_UPD_CASE(3)
@@ -1398,75 +1579,6 @@ hipError_t launch_step_update(const dgprf_plan_t& pl, const StepDev& sd, const U
   return hipGetLastError();
 }
 
-hipError_t launch_step_hyper(const dgprf_plan_t& pl, const StepDev& sd, const UpdateDev& ud,
-                             hipStream_t s) {
-  HypK a;
-  a.hyp = sd.hyp;
-  a.hmom = sd.hmom;
-  a.hmass = sd.hmass;
-  a.z = sd.z;
-  a.omega = sd.omega;
-  a.der = sd.der;
-  a.ws = sd.ws;
-  a.step = sd.step;
-  a.grad_out = sd.grad_out;
-  a.seed = sd.seed;
-  a.ws_cs = pl.ws_chain;
-  a.hyp_cs = sd.hyp_cs;
-  a.om_cs = sd.om_cs;
-  a.der_cs = sd.der_cs;
-  a.hyp_total = pl.hyp_total;
-  a.grad_cs = pl.w_total + pl.hyp_total;
-  a.w_total = pl.w_total;
-  a.n_layers = pl.n_layers;
-  a.n_rt = pl.n_row_tiles;
-  a.step_offset = sd.step_offset;
-  a.flags = pl.hyp_flags;
-  a.likelihood = pl.likelihood;
-  int hsmax = 4, pmax = 1;
-  for (int l = 0; l < DGPRF_MAX_LAYERS; ++l) {
-    const bool on = l < pl.n_layers;
-    a.d[l] = on ? pl.d[l] : 0;
-    a.R[l] = on ? pl.n_rf[l] : 0;
-    a.kind[l] = on ? pl.kind[l] : 0;
-    a.ard[l] = on ? pl.ard[l] : 0;
-    a.ns[l] = on ? pl.ns[l] : 0;
-    a.lis_off[l] = on ? pl.lis_off[l] : 0;
-    a.mean_off[l] = on ? pl.mean_off[l] : 0;
-    a.om_off[l] = on ? pl.omega_off[l] : 0;
-    a.hpp_off[l] = on ? pl.hpp_off[l] : 0;
-    if (on) {
-      hsmax = max(hsmax, round4(2 * pl.d[l] + 1));
-      pmax = max(pmax, pl.n_row_tiles * pl.ns[l]);
-    }
-  }
-  a.hpl_off = pl.hpl_off;
-  a.ud = ud;
-  // value tile staged in LDS: [P][vt] partial rows, vt a multiple of 4 within ~128 KB
-  int vt = (32768 - hsmax - 256) / pmax;
-  vt = vt > 64 ? 64 : (vt & ~3);
-  if (vt < 4) return hipErrorInvalidValue;
-  a.vt = vt;
-  const size_t lds = (size_t)(pmax * vt + hsmax + 256) * sizeof(float);
-  dim3 grid(pl.n_layers + 1, pl.n_chains);
-  const bool gonly = ud.grad_only != 0, xi = ud.xi_hyp || ud.xi_hyp_resample;
-  const bool cyc = ud.schedule == DGPRF_SCHED_CYCLICAL;
-#define DGPRF_HYP(G_, X_, C_)                                                   \
-  do {                                                                         \
-    dgprf::set_lds_limit((const void*)k_step_hyper<G_, X_, C_>, lds);          \
-    hipLaunchKernelGGL((k_step_hyper<G_, X_, C_>), grid, dim3(256), lds, s, a); \
-  } while (0)
-  if (gonly) DGPRF_HYP(true, false, false);
-  else if (xi) {
-    if (cyc) DGPRF_HYP(false, true, true);
-    else DGPRF_HYP(false, true, false);
-  } else {
-    if (cyc) DGPRF_HYP(false, false, true);
-    else DGPRF_HYP(false, false, false);
-  }
-#undef DGPRF_HYP
-  return hipGetLastError();
-}
 
 hipError_t launch_gather(const dgprf_plan_t& pl, const StepDev& sd, hipStream_t s) {
   if (sd.bd.mode == DGPRF_BATCH_DIRECT) return hipSuccess;

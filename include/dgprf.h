@@ -90,7 +90,9 @@ extern "C" {
  *   der             [der_total]          : c_l = amp/sqrt(R) (RBF) or sqrt2*amp/sqrt(R) (ARC),
  *                                          then sigma^2 at der[DGPRF_MAX_LAYERS]
  *   mass            [n_chains][n_layers] : preconditioner M per W_l (models/dgp.py:235-237)
- *   workspace       [ws_total]           : step-kernel partials (per chain ws_chain floats)
+ *   workspace       [ws_total]           : step-kernel partials (per chain ws_chain floats); zero-fill
+ *                                          it once before first use (it holds the full-Bayes
+ *                                          arrival counters, which the kernels leave at zero)
  */
 typedef struct dgprf_plan {
   /* ---- caller ---- */
@@ -130,7 +132,8 @@ typedef struct dgprf_plan {
   int64_t ws_chain;
   int64_t ws_total;
   int64_t hpp_off[DGPRF_MAX_LAYERS]; /* full-Bayes partials [n_rt_pad][16][align4(2 d_l + 1)] (per chain) */
-  int64_t hpl_off;                   /* full-Bayes lik_log_var partials [n_rt_pad] (per chain)  */
+  int64_t hpl_off;                   /* full-Bayes lik_log_var partials [n_rt_pad], then 8 uint32
+                                        arrival counters of the hyper workgroups (per chain)   */
   int64_t xb_off;                    /* gathered minibatch rows X [B][d_in] (per chain)        */
   int64_t yb_off;                    /* gathered minibatch targets [B][yb_cols] (per chain)    */
   int32_t yb_cols;                   /* g_L (Gaussian) or 1 (softmax label)                    */

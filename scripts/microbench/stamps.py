@@ -24,15 +24,16 @@ SLOTS = 16
 dev = torch.device("cuda", 0)
 X, Y, _ = regression_data(1_000_000, 8, 0, device=dev)
 m = RegressionDGP(8, 1, n_hidden_layers=3, n_rf=1024, n_gp=[8, 8, 1], likelihood=Gaussian())
-m.precond_update(None, 1_000_000, precond_type="identity")
+FB = "--full-bayes" in sys.argv  # full_bayesian=True steps; hyper workgroups reported apart
+m.precond_update(None, 1_000_000, precond_type="identity", full_bayesian=FB)
 eng = m._engine
 lib = N.lib()
 for _ in range(50):
-    eng.step(X, Y, 1_000_000, 0.01, 0.9, 1.0, batch_size=200, mode=2)
+    eng.step(X, Y, 1_000_000, 0.01, 0.9, 1.0, batch_size=200, mode=2, full_bayes=FB)
 torch.cuda.synchronize()
 lib.dgprf_debug_clear_stamps()
 for _ in range(3):
-    eng.step(X, Y, 1_000_000, 0.01, 0.9, 1.0, batch_size=200, mode=2)
+    eng.step(X, Y, 1_000_000, 0.01, 0.9, 1.0, batch_size=200, mode=2, full_bayes=FB)
 torch.cuda.synchronize()
 n = 17 * 4096 * SLOTS
 buf = (ctypes.c_ulonglong * n)()
@@ -40,10 +41,18 @@ assert lib.dgprf_debug_read_stamps(buf, n) == 0
 S = np.frombuffer(buf, dtype=np.uint64).reshape(17, 4096, SLOTS).astype(np.int64)
 names = {0: "fwd0", 2: "fwd1", 4: "fwd2", 1: "bwd0", 3: "bwd1", 5: "bwd2", 16: "update"}
 order = [0, 2, 4, 5, 3, 1, 16]
+if FB:  # the update kernel's first workgroups are the hyper ones (one per 1024 Omega elements + 1)
+    pl = eng.layout
+    n_hyp = sum((pl.d[l] * pl.n_rf[l] + 1023) // 1024 for l in range(eng.L)) + 1
+    S = np.concatenate([S, S[16:17]], axis=0)
+    S[17, n_hyp:] = 0
+    S[16, :n_hyp] = 0
+    names[17] = "hyper"
+    order.append(17)
 t0_all = []
 for k in order:
     st = S[k]
-    valid = st[:, 0] > 0
+    valid = (st[:, 0] > 0) & (st[:, 14] > 0)
     st = st[valid]
     if len(st) == 0:
         continue
