@@ -24,6 +24,13 @@ __device__ __forceinline__ f4 mfma16(float a, float b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// v_mfma_f32_4x4x1_16b_f32: 16 independent 4x4x1 blocks, block b = lanes 4b..4b+3 (measured,
+// scripts/microbench/mfma4x4.hip):  A_b[i] = lane 4b+i,  B_b[j] = lane 4b+j,  D_b[i][j] = lane 4b+j
+// reg i.  256 MACs per ~8-12 cycles: the fit for contractions whose output width is <= 8.
+__device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 0, 0, 0);
+}
+
 __device__ __forceinline__ f4 f4zero() {
   f4 z = {0.f, 0.f, 0.f, 0.f};
   return z;

@@ -404,6 +404,9 @@ constexpr int TW_ROWS = NW * TR;  // rows per workgroup
 #ifndef DGPRF_TILE_TPW_DEFAULT
 #define DGPRF_TILE_TPW_DEFAULT 1  // 16-row tiles per wave (2: two chains per wave, but 186 VGPRs -> 2 waves/SIMD, slower)
 #endif
+#ifndef DGPRF_TILE_G8
+#define DGPRF_TILE_G8 1  // layers with 2 <= g <= 8: F contraction on 4x4x1 MFMA blocks (no padding)
+#endif
 constexpr int TW_OST = 80;        // LDS row stride of a staged Omega block (conflict-free reads)
 __host__ __device__ constexpr int tw_wst(int notm) { return 16 * notm + 4; }  // W row stride
 
@@ -434,13 +437,15 @@ __host__ __device__ inline TileLds tile_lds(const dgprf_plan_t& pl, int notmax, 
 // WST = 16 NOT + 4 (g == 1: raw [h][64]); feature rows >= R are zeroed while staging, and output
 // columns o >= g are never stored, so the fragment reads need neither masks nor clamps and all
 // their offsets are immediates.
-template <int NOT, bool RBF, bool G1, int JW, int JO, int KS, int TPW>
+template <int NOT, bool RBF, bool G1, bool G8, int JW, int JO, int KS, int TPW>
 __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
                                            const float* __restrict__ W,
                                            const float* __restrict__ om, float cl,
                                            const TileLds& T, float* smem, float* xin, float* ftw,
                                            int lr, int lq, int64_t wrow0, int64_t n, float* fout) {
-  constexpr int WST = tw_wst(NOT);
+  // G8 (2 <= g <= 8): W rows of 8 with the columns interleaved as 2 (o & 3) + (o >> 2), so a lane's
+  // two 4x4-block operands (o = i, 4 + i) are one ds_read_b64
+  constexpr int WST = G8 ? 8 : tw_wst(NOT);
   constexpr bool REV = RBF && !DGPRF_PRECISE_TRIG_ON;
   // the k-steps read Omega rows 0..4KS-1 of the staged block: all of them must be staged (rows >= d
   // as zeros) — LDS is not cleared between kernels, and 0 * stale NaN is NaN
@@ -489,6 +494,13 @@ __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
 #pragma unroll
           for (int t = 0; t < 4; ++t) v[t] = fb + e0 + t < R ? v[t] : 0.f;
           *reinterpret_cast<f4*>(wsb + h * 64 + e0) = v;
+        } else if (G8) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const int e = e0 + t, row = (e * gmag) >> 20, col = e - row * g;
+            if (row < 64)
+              wsb[(h * 64 + row) * WST + 2 * (col & 3) + (col >> 2)] = fb + row < R ? sw[j][t] : 0.f;
+          }
         } else if ((g & 3) == 0) {  // the float4 lies in one row
           const int row = (e0 * gmag) >> 20, col = e0 - row * g;
           const f4 v = fb + row < R ? sw[j] : f4zero();
@@ -511,12 +523,15 @@ __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
   };
 
   f4 acc[TPW][NOT], acs[TPW][NOT];
+  // G8: 4x4-block accumulators [t][h]: lane (lq, lr) reg i = F[row lr][4h + i] over features 4lq..
+  f4 a8[TPW][2], s8[TPW][2];
   float dot[TPW];
 #pragma unroll
   for (int t = 0; t < TPW; ++t) {
     dot[t] = 0.f;
 #pragma unroll
     for (int ot = 0; ot < NOT; ++ot) acc[t][ot] = acs[t][ot] = f4zero();
+    a8[t][0] = a8[t][1] = s8[t][0] = s8[t][1] = f4zero();
   }
   const int nb = (R + 63) >> 6;
   stage_load(0);
@@ -527,7 +542,7 @@ __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
     if (blk + 1 < nb) stage_load(fb + 64);
     const float* wsb = smem + T.w_off + buf * T.wbuf;
     const float* osb = smem + T.o_off + buf * T.obuf + lq * TW_OST + lr;
-    const float* wl = wsb + (G1 ? 4 * lq : 4 * lq * WST + lr);
+    const float* wl = wsb + (G1 ? 4 * lq : (G8 ? 4 * lq * WST + 2 * (lr & 3) : 4 * lq * WST + lr));
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       // A[tile t, row lr][feature fb + 16c + 4lq + r]; the Omega / W fragments serve every tile
@@ -548,9 +563,14 @@ __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           if (REV) {
+#ifdef DGPRF_EXP_NOTRIG
+            p0[t][r] = at[t][r];
+            p1[t][r] = at[t][r] * 0.5f;
+#else
             const float u = __builtin_amdgcn_fractf(at[t][r]);
             p0[t][r] = __builtin_amdgcn_cosf(u);
             p1[t][r] = __builtin_amdgcn_sinf(u);
+#endif
           } else if (RBF) {
             float sv, cv;
             rf_sincos(at[t][r], &sv, &cv);
@@ -571,6 +591,25 @@ __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
             dot[t] = fmaf(p0[t][r], w0[r], dot[t]);
             if (RBF) dot[t] = fmaf(p1[t][r], w1[r], dot[t]);
           }
+      } else if (G8) {
+        // 4x4x1 blocks: block b = 4 lq + (lr >> 2) covers rows 4 (b & 3) + j and feature 4 lq + r;
+        // A = W[feature][4h + (lr & 3)], B = this lane's cos / sin value
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          typedef float f2v __attribute__((ext_vector_type(2)));
+          const f2v wc = *reinterpret_cast<const f2v*>(wl + (16 * c + r) * WST);
+          f2v wsn = {0.f, 0.f};
+          if (RBF) wsn = *reinterpret_cast<const f2v*>(wl + (64 + 16 * c + r) * WST);
+#pragma unroll
+          for (int t = 0; t < TPW; ++t) {
+            a8[t][0] = mfma4(wc[0], p0[t][r], a8[t][0]);
+            a8[t][1] = mfma4(wc[1], p0[t][r], a8[t][1]);
+            if (RBF) {
+              s8[t][0] = mfma4(wsn[0], p1[t][r], s8[t][0]);
+              s8[t][1] = mfma4(wsn[1], p1[t][r], s8[t][1]);
+            }
+          }
+        }
       } else {
 #pragma unroll
         for (int ot = 0; ot < NOT; ++ot)
@@ -581,8 +620,13 @@ __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
             const float w1 = RBF ? wl[64 * WST + off] : 0.f;
 #pragma unroll
             for (int t = 0; t < TPW; ++t) {
+#ifdef DGPRF_EXP_NOFMFMA
+              acc[t][ot][r] = fmaf(w0, p0[t][r], acc[t][ot][r]);
+              if (RBF) acs[t][ot][r] = fmaf(w1, p1[t][r], acs[t][ot][r]);
+#else
               acc[t][ot] = mfma16(w0, p0[t][r], acc[t][ot]);
               if (RBF) acs[t][ot] = mfma16(w1, p1[t][r], acs[t][ot]);
+#endif
             }
           }
       }
@@ -604,6 +648,22 @@ __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
         ftw[row * T.ftst] = v;
         if (fout && b < n) fout[b] = v;
       }
+    } else if (G8) {
+      // sum the four feature groups (lanes lr, lr + 16, lr + 32, lr + 48)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float v = a8[t][h][i] + s8[t][h][i];
+          v += __shfl_xor(v, 16);
+          v += __shfl_xor(v, 32);
+          const int o = 4 * h + i;
+          if (lq == 0 && o < g) {
+            v *= cl;
+            ftw[row * T.ftst + o] = v;
+            if (fout && b < n) fout[b * g + o] = v;
+          }
+        }
     } else {
       // acc[t][ot][r] = F[tile t, row lr][ot*16 + 4lq + r] / c
 #pragma unroll
@@ -656,27 +716,30 @@ void k_forward_tiles(
     const int g = pl.n_gp[layer], NOT = (g + 15) >> 4;
     const bool rbf = pl.kind[layer] == DGPRF_RBF, ks2 = pl.d[layer] <= 8;
     float* fout = fo.p[layer] ? fo.p[layer] + (int64_t)chain * n * g : nullptr;
-#define DGPRF_TL(NT, RB, G1_)                                                                       \
+#define DGPRF_TL(NT, RB, G1_, G8_)                                                                     \
   do {                                                                                              \
     if (ks2)                                                                                        \
-      tile_layer<NT, RB, G1_, JW, JO, 2, TPW>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, n, \
-                                         fout);                                                     \
+      tile_layer<NT, RB, G1_, G8_, JW, JO, 2, TPW>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, \
+                                              n, fout);                                             \
     else                                                                                            \
-      tile_layer<NT, RB, G1_, JW, JO, 4 * JO, TPW>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, n, \
-                                         fout);                                                     \
+      tile_layer<NT, RB, G1_, G8_, JW, JO, 4 * JO, TPW>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq,  \
+                                                   wrow0, n, fout);                                 \
   } while (0)
     if (g == 1) {
-      if (rbf) DGPRF_TL(1, true, true);
-      else DGPRF_TL(1, false, true);
+      if (rbf) DGPRF_TL(1, true, true, false);
+      else DGPRF_TL(1, false, true, false);
+    } else if (DGPRF_TILE_G8 && g <= 8) {
+      if (rbf) DGPRF_TL(1, true, false, true);
+      else DGPRF_TL(1, false, false, true);
     } else if (NOT == 1) {
-      if (rbf) DGPRF_TL(1, true, false);
-      else DGPRF_TL(1, false, false);
+      if (rbf) DGPRF_TL(1, true, false, false);
+      else DGPRF_TL(1, false, false, false);
     } else if (NOTMAX >= 2 && NOT == 2) {
-      if (rbf) DGPRF_TL((NOTMAX >= 2 ? 2 : 1), true, false);
-      else DGPRF_TL((NOTMAX >= 2 ? 2 : 1), false, false);
+      if (rbf) DGPRF_TL((NOTMAX >= 2 ? 2 : 1), true, false, false);
+      else DGPRF_TL((NOTMAX >= 2 ? 2 : 1), false, false, false);
     } else if (NOTMAX >= 4) {
-      if (rbf) DGPRF_TL((NOTMAX >= 4 ? 4 : 1), true, false);
-      else DGPRF_TL((NOTMAX >= 4 ? 4 : 1), false, false);
+      if (rbf) DGPRF_TL((NOTMAX >= 4 ? 4 : 1), true, false, false);
+      else DGPRF_TL((NOTMAX >= 4 ? 4 : 1), false, false, false);
     }
 #undef DGPRF_TL
   }

@@ -347,6 +347,50 @@ class DGP_RF(Module):
         else:
             raise NotImplementedError
 
+    # ------------------------------------------------------------------ MCEM M-step
+    def hyper_variables(self):
+        """The variables MCEM_Q_maximizer watches: Omega_hyperparams + Likelihood_hyperparams
+        (experiments/utils_training.py:342), in that order."""
+        return list(self.Omega_hyperparams) + list(self.Likelihood_hyperparams)
+
+    def Q_and_hyper_grads(self, W_samples, X_batch, Y_batch, data_size):
+        """Q = (1/S) sum_s -U(W_s; full_bayesian=False, allow_gradient_from_W=False) and
+        d(-Q)/d(hyper) for hyper_variables() (experiments/utils_training.py:339-358).
+
+        -U without the W prior is the minibatch log-likelihood, so d(-Q)/d(hyper) is the device
+        full-Bayes hyper-parameter gradient (k_step_bwd<FB> + the hyper reduction) minus its prior
+        term hyper/N, averaged over the samples.  Each sample is assign_W'd first; the model is
+        left holding the last one, like the reference's loop.  Returns (Q, grads)."""
+        eng = self._engine
+        pl = eng.layout
+        X_batch = E.as_device(X_batch, eng.dev)
+        Y_batch = E.as_device(Y_batch, eng.dev)
+        B = float(X_batch.shape[0])
+        acc = torch.zeros(pl.hyp_total, dtype=torch.float32, device=eng.dev)
+        Q = torch.zeros((), dtype=torch.float32, device=eng.dev)
+        S = 0
+        for W_model_list in W_samples:
+            self.assign_W(W_model_list)
+            om, z = self._omega_and_z_for_call()
+            g = eng.grad(X_batch, Y_batch, data_size, build=False, omega=om, z=z,
+                         full_bayes=True)
+            acc += g[0, pl.w_total:]
+            Q += torch.sum(eng.forward(X_batch, Y_batch, logp=True, omega=om,
+                                       build=False)["logp"][0]) / B
+            S += 1
+        acc /= S
+        by_var = {id(v): (o, n) for v, _, o, n in self._hyper_vars()}
+        grads = []
+        for v in self.hyper_variables():
+            o, n = by_var[id(v)]
+            grads.append(acc[o:o + n].view(v.shape) - v.detach() / float(data_size))
+        return Q / S, grads
+
+    def collect_W(self):
+        """{'W_l': copy of GP layer l's W} — the helper experiments/utils_training_demo.py:57,140
+        calls (absent from the reference's models/)."""
+        return {'W_' + str(i): W.detach().clone() for i, W in enumerate(self.W_mcmc)}
+
     def set_random_fixed(self, state):
         for l in range(self.n_hidden_layers):
             self.BNN.layers[2 * l].set_random_fixed(state)

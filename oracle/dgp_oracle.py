@@ -402,3 +402,58 @@ def predictive_summary(log_p, se, y_std=1.0):
     ll = np.mean(lse - np.log(S))
     rmse = np.sqrt(np.mean(np.asarray(se, dtype=np.float64) * y_std ** 2))
     return ll, rmse
+
+
+# ----------------------------------------------------------------------------- MCEM M-step
+def q_function_and_grad(p, W_samples, X, Y, N, tr):
+    """MCEM_Q_maximizer (experiments/utils_training.py:339-358, utils_training_demo.py:171-191):
+    Q = (1/S) sum_s -U(W_s; full_bayesian=False, allow_gradient_from_W=False)
+      = (1/S) sum_s (1/B) sum_b log p(y_b | x_b, W_s)        (no prior: dgp.py:169-174)
+    and d(-Q)/d(hyper) for the watched Omega_hyperparams + Likelihood_hyperparams, which is the
+    full-Bayes hyper-parameter gradient of grad_full without its prior term hyper/N.
+    W_samples: list over S of per-layer W lists.  Returns (Q, dict like grad_full minus 'W');
+    p.W is left at the last sample (the reference's assign_W leaves it there too)."""
+    X = np.asarray(X, dtype=p.dtype)
+    B = X.shape[0]
+    Q = 0.0
+    acc = None
+    for Ws in W_samples:
+        p.W = [np.asarray(w, dtype=p.dtype).copy() for w in Ws]
+        Q += np.sum(log_prob(p, forward(p, X), Y)) / B
+        g = grad_full(p, X, Y, N, tr)
+        g.pop("W")
+        if acc is None:
+            acc = g
+            continue
+        for k in ("log_amp", "log_inv_ls", "mean"):
+            acc[k] = [a if a is None else a + b for a, b in zip(acc[k], g[k])]
+        if acc["lik_log_var"] is not None:
+            acc["lik_log_var"] = acc["lik_log_var"] + g["lik_log_var"]
+    S = len(W_samples)
+    out = {"log_amp": [None] * p.L, "log_inv_ls": [None] * p.L, "mean": [None] * p.L,
+           "lik_log_var": None}
+    for l in range(p.L):
+        if acc["log_amp"][l] is not None:
+            out["log_amp"][l] = acc["log_amp"][l] / S - p.log_amp[l] / N
+        if acc["log_inv_ls"][l] is not None:
+            ard = tr.ard is None or tr.ard[l]
+            lis = p.log_inv_ls[l] if ard else p.log_inv_ls[l][0]
+            out["log_inv_ls"][l] = acc["log_inv_ls"][l] / S - lis / N
+        if acc["mean"][l] is not None:
+            out["mean"][l] = acc["mean"][l] / S - p.mean[l] / N
+    if acc["lik_log_var"] is not None:
+        out["lik_log_var"] = acc["lik_log_var"] / S - p.lik_log_var / N
+    return Q / S, out
+
+
+def adam_update(var, g, m, v, t, lr=0.001, beta_1=0.9, beta_2=0.999, epsilon=1e-7):
+    """One tf.keras.optimizers.Adam step (the optimizer the reference's MCEM notebooks pass to
+    MCEM_Q_maximizer, experiments/train_classification.ipynb cell 'optimizer = optimizers.Adam',
+    defaults of TF2 Keras Adam):  t = iteration (from 1),
+      lr_t = lr sqrt(1 - beta_2^t) / (1 - beta_1^t),  m <- beta_1 m + (1 - beta_1) g,
+      v <- beta_2 v + (1 - beta_2) g^2,  var <- var - lr_t m / (sqrt(v) + epsilon).
+    Returns (var, m, v)."""
+    lr_t = lr * np.sqrt(1.0 - beta_2 ** t) / (1.0 - beta_1 ** t)
+    m = beta_1 * m + (1.0 - beta_1) * g
+    v = beta_2 * v + (1.0 - beta_2) * g * g
+    return var - lr_t * m / (np.sqrt(v) + epsilon), m, v
