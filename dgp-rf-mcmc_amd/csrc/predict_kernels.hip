@@ -404,6 +404,9 @@ constexpr int TW_ROWS = NW * TR;  // rows per workgroup
 #ifndef DGPRF_TILE_TPW_DEFAULT
 #define DGPRF_TILE_TPW_DEFAULT 1  // 16-row tiles per wave (2: two chains per wave, but 186 VGPRs -> 2 waves/SIMD, slower)
 #endif
+#ifndef DGPRF_TILE_APHASE
+#define DGPRF_TILE_APHASE 1  // issue a block's four A-tile chains before its trig / F work
+#endif
 #ifndef DGPRF_TILE_G8
 #define DGPRF_TILE_G8 1  // layers with 2 <= g <= 8: F contraction on 4x4x1 MFMA blocks (no padding)
 #endif
@@ -447,6 +450,7 @@ __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
   // two 4x4-block operands (o = i, 4 + i) are one ds_read_b64
   constexpr int WST = G8 ? 8 : tw_wst(NOT);
   constexpr bool REV = RBF && !DGPRF_PRECISE_TRIG_ON;
+  constexpr bool APHASE = DGPRF_TILE_APHASE && KS <= 2;
   // the k-steps read Omega rows 0..4KS-1 of the staged block: all of them must be staged (rows >= d
   // as zeros) — LDS is not cleared between kernels, and 0 * stale NaN is NaN
   static_assert(4 * KS <= 16 * JO, "k-steps beyond the staged Omega rows");
@@ -543,18 +547,40 @@ __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
     const float* wsb = smem + T.w_off + buf * T.wbuf;
     const float* osb = smem + T.o_off + buf * T.obuf + lq * TW_OST + lr;
     const float* wl = wsb + (G1 ? 4 * lq : (G8 ? 4 * lq * WST + 2 * (lr & 3) : 4 * lq * WST + lr));
+    // A[tile t, row lr][feature fb + 16c + 4lq + r]; the Omega / W fragments serve every tile.
+    // APHASE: the four chunks' A tiles are issued together first (independent MFMA chains, so their
+    // dependent latency overlaps), and the trig + F contraction of chunk c follows.
+    f4 atc[APHASE ? 4 : 1][TPW];
+    if (APHASE) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float om[KS];
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) om[ks] = osb[4 * ks * TW_OST + 16 * c];
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+          atc[c][t] = f4zero();
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks) atc[c][t] = mfma16(om[ks], xf[t][ks], atc[c][t]);
+        }
+      }
+    }
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      // A[tile t, row lr][feature fb + 16c + 4lq + r]; the Omega / W fragments serve every tile
-      float om[KS];
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) om[ks] = osb[4 * ks * TW_OST + 16 * c];
       f4 at[TPW];
+      if (APHASE) {
 #pragma unroll
-      for (int t = 0; t < TPW; ++t) {
-        at[t] = f4zero();
+        for (int t = 0; t < TPW; ++t) at[t] = atc[c][t];
+      } else {
+        float om[KS];
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) at[t] = mfma16(om[ks], xf[t][ks], at[t]);
+        for (int ks = 0; ks < KS; ++ks) om[ks] = osb[4 * ks * TW_OST + 16 * c];
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+          at[t] = f4zero();
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks) at[t] = mfma16(om[ks], xf[t][ks], at[t]);
+        }
       }
       // features without the scale c (applied once to F): cos/sin(A) or relu(A)
       float p0[TPW][4], p1[TPW][4];
