@@ -397,7 +397,17 @@ __global__ __launch_bounds__(256) void k_prior_w(const dgprf_plan_t pl,
 //     per block;
 //   * the layer output F (16 x g per wave) stays in the wave's LDS tile and is the next layer's
 //     input; dataset columns ([F | X], utils.py:42) come from the wave's X rows, loaded once.
-constexpr int TW_ROWS = NW * TR;  // rows per workgroup
+#ifndef DGPRF_TILE_WG_WAVES
+// waves per workgroup (4 waves = 4 SIMDs).  16 (one workgroup per CU) makes the per-block barrier
+// keep the 4 waves of each SIMD in step — otherwise oldest-first issue arbitration starves the
+// younger waves and the last ones finish alone — but measured no faster at N_t = 1e5 (lockstep
+// phases overlap MFMA and VALU worse, and 1.5 rounds of 16-tile workgroups leave half the CUs idle
+// in the second); DESIGN.md §4.
+#define DGPRF_TILE_WG_WAVES 4
+#endif
+constexpr int TWW = DGPRF_TILE_WG_WAVES;
+constexpr int TW_THREADS = 64 * TWW;
+constexpr int TW_ROWS = TWW * TR;  // rows per workgroup
 #ifndef DGPRF_TILE_WAVES
 #define DGPRF_TILE_WAVES 4  // waves per SIMD the register budget must allow (latency hiding)
 #endif
@@ -406,6 +416,9 @@ constexpr int TW_ROWS = NW * TR;  // rows per workgroup
 #endif
 #ifndef DGPRF_TILE_APHASE
 #define DGPRF_TILE_APHASE 1  // issue a block's four A-tile chains before its trig / F work
+#endif
+#ifndef DGPRF_TILE_G8MIX
+#define DGPRF_TILE_G8MIX 0  // 1: G8 RBF cos half on 16x16x4 tiles (measured slower: 241 vs 221 us)
 #endif
 #ifndef DGPRF_TILE_G8
 #define DGPRF_TILE_G8 1  // layers with 2 <= g <= 8: F contraction on 4x4x1 MFMA blocks (no padding)
@@ -428,8 +441,8 @@ __host__ __device__ inline TileLds tile_lds(const dgprf_plan_t& pl, int notmax, 
   T.xin_st = round4(pl.d_in);
   T.xin_off = T.w_off + 2 * T.wbuf;
   T.ftst = gmax + 1;
-  T.f_off = T.xin_off + NW * tpw * TR * T.xin_st;
-  T.total = T.f_off + NW * round4(tpw * TR * T.ftst);
+  T.f_off = T.xin_off + TWW * tpw * TR * T.xin_st;
+  T.total = T.f_off + TWW * round4(tpw * TR * T.ftst);
   return T;
 }
 
@@ -473,7 +486,9 @@ __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
   const rsrc_t ro = make_rsrc(om, (int64_t)d * R);
   const int nwq = (RBF ? 32 : 16) * g;  // float4 of one W block
   f4 sw[JW], so[JO];
+  const bool stager = tid < 256;  // the staging counts JW / JO are per 256 threads
   auto stage_load = [&](int fb) {
+    if (!stager) return;
 #pragma unroll
     for (int j = 0; j < JW; ++j) {
       const int i = tid + 256 * j, h = i >= 16 * g, q = i - h * 16 * g;
@@ -486,6 +501,7 @@ __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
     }
   };
   auto stage_store = [&](int buf, int fb) {
+    if (!stager) return;
     float* wsb = smem + T.w_off + buf * T.wbuf;
     float* osb = smem + T.o_off + buf * T.obuf;
 #pragma unroll
@@ -547,6 +563,8 @@ __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
     const float* wsb = smem + T.w_off + buf * T.wbuf;
     const float* osb = smem + T.o_off + buf * T.obuf + lq * TW_OST + lr;
     const float* wl = wsb + (G1 ? 4 * lq : (G8 ? 4 * lq * WST + 2 * (lr & 3) : 4 * lq * WST + lr));
+    // G8 + MIX: W^T operand of the 16x16x4 cos tiles, row o = lr (interleaved column)
+    const float* wl16 = wsb + 4 * lq * WST + 2 * (lr & 3) + ((lr >> 2) & 1);
     // A[tile t, row lr][feature fb + 16c + 4lq + r]; the Omega / W fragments serve every tile.
     // APHASE: the four chunks' A tiles are issued together first (independent MFMA chains, so their
     // dependent latency overlaps), and the trig + F contraction of chunk c follows.
@@ -619,17 +637,28 @@ __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
           }
       } else if (G8) {
         // 4x4x1 blocks: block b = 4 lq + (lr >> 2) covers rows 4 (b & 3) + j and feature 4 lq + r;
-        // A = W[feature][4h + (lr & 3)], B = this lane's cos / sin value
+        // A = W[feature][4h + (lr & 3)], B = this lane's cos / sin value.
+        // MIX (RBF): the cos half stays on 16x16x4 tiles (rows o >= 8 of the A operand read other
+        // columns; their outputs are never used) — 4x4 blocks are cheap in the matrix pipe but hold
+        // the SIMD's issue port, so the two forms are split to balance the two limits.
+        constexpr bool MIX = RBF && DGPRF_TILE_G8MIX;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           typedef float f2v __attribute__((ext_vector_type(2)));
-          const f2v wc = *reinterpret_cast<const f2v*>(wl + (16 * c + r) * WST);
+          f2v wc = {0.f, 0.f};
+          float wc16 = 0.f;
+          if (MIX) wc16 = wl16[(16 * c + r) * WST];
+          else wc = *reinterpret_cast<const f2v*>(wl + (16 * c + r) * WST);
           f2v wsn = {0.f, 0.f};
           if (RBF) wsn = *reinterpret_cast<const f2v*>(wl + (64 + 16 * c + r) * WST);
 #pragma unroll
           for (int t = 0; t < TPW; ++t) {
-            a8[t][0] = mfma4(wc[0], p0[t][r], a8[t][0]);
-            a8[t][1] = mfma4(wc[1], p0[t][r], a8[t][1]);
+            if (MIX) {
+              acc[t][0] = mfma16(wc16, p0[t][r], acc[t][0]);
+            } else {
+              a8[t][0] = mfma4(wc[0], p0[t][r], a8[t][0]);
+              a8[t][1] = mfma4(wc[1], p0[t][r], a8[t][1]);
+            }
             if (RBF) {
               s8[t][0] = mfma4(wsn[0], p1[t][r], s8[t][0]);
               s8[t][1] = mfma4(wsn[1], p1[t][r], s8[t][1]);
@@ -676,6 +705,7 @@ __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
       }
     } else if (G8) {
       // sum the four feature groups (lanes lr, lr + 16, lr + 32, lr + 48)
+      constexpr bool MIX = RBF && DGPRF_TILE_G8MIX;
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -684,7 +714,9 @@ __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
           v += __shfl_xor(v, 16);
           v += __shfl_xor(v, 32);
           const int o = 4 * h + i;
-          if (lq == 0 && o < g) {
+          // MIX: the 16x16x4 cos tile holds F^T[o = 4 lq + i][row lr] in lane group lq = h
+          if ((MIX ? lq == h : lq == 0) && o < g) {
+            if (MIX) v += acc[t][0][i];
             v *= cl;
             ftw[row * T.ftst + o] = v;
             if (fout && b < n) fout[b * g + o] = v;
@@ -708,8 +740,25 @@ __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
   __syncthreads();  // ftw complete before the next layer reads its x fragments
 }
 
+// Per-wave timeline of the tile kernel for a separate diagnostic build (-DDGPRF_PSTAMPS, never in
+// the product): slot 0 = s_memrealtime at entry, 7 = s_memtime at entry, 1..4 = s_memtime after
+// each layer, 6 = s_memrealtime at exit, 5 = HW_ID | XCC_ID << 32.
+#ifdef DGPRF_PSTAMPS
+__device__ unsigned long long g_pred_stamps[1 << 20];
+#define DGPRF_PST(i, v)                                                        \
+  do {                                                                         \
+    const int64_t wid_ = (int64_t)blockIdx.x * TWW + (threadIdx.x >> 6);       \
+    if ((threadIdx.x & 63) == 0 && wid_ * 8 + 7 < (1 << 20))                   \
+      g_pred_stamps[wid_ * 8 + (i)] = (v);                                     \
+  } while (0)
+#else
+#define DGPRF_PST(i, v) \
+  do {                  \
+  } while (0)
+#endif
+
 template <int NOTMAX, int JW, int JO, int TPW>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? DGPRF_TILE_WAVES : 2)))
+__global__ __launch_bounds__(TW_THREADS) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? DGPRF_TILE_WAVES : 2)))
 void k_forward_tiles(
     const dgprf_plan_t pl, const float* __restrict__ theta, const float* __restrict__ omega,
     const float* __restrict__ der, const float* __restrict__ X, const float* __restrict__ Y,
@@ -727,6 +776,10 @@ void k_forward_tiles(
   float* ftw = smem + T.f_off + wave * round4(TPW * TR * T.ftst);
   const float* Wc = theta + (int64_t)chain * pl.w_total;
   const int L = pl.n_layers;
+  DGPRF_PST(0, __builtin_amdgcn_s_memrealtime());
+  DGPRF_PST(7, __builtin_amdgcn_s_memtime());
+  DGPRF_PST(5, (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4) |
+                   ((unsigned long long)__builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20) << 32));
   // this wave's X rows (zero past n)
   for (int e = lane; e < TPW * TR * T.xin_st; e += 64) {
     const int r = e / T.xin_st, k = e - r * T.xin_st;
@@ -768,6 +821,7 @@ void k_forward_tiles(
       else DGPRF_TL((NOTMAX >= 4 ? 4 : 1), false, false, false);
     }
 #undef DGPRF_TL
+    if (layer < 4) DGPRF_PST(1 + layer, __builtin_amdgcn_s_memtime());
   }
   // likelihood per row: lanes 0..15 of each wave, row lr of each of the wave's tiles
   const bool want_lik = logp_out || se_out || lse_m;
@@ -807,9 +861,17 @@ void k_forward_tiles(
       }
     }
   }
+  DGPRF_PST(6, __builtin_amdgcn_s_memrealtime());
 }
 
 }  // namespace
+
+#ifdef DGPRF_PSTAMPS
+extern "C" int dgprf_debug_read_pred_stamps(unsigned long long* host, long long n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pred_stamps), (size_t)n * 8, 0,
+                             hipMemcpyDeviceToHost);
+}
+#endif
 
 namespace dgprf {
 
@@ -852,11 +914,11 @@ hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const
   do {                                                                                             \
     if (tpw == 2) {                                                                                \
       set_lds_limit((const void*)k_forward_tiles<NM, J, JO, 2>, tl);                               \
-      hipLaunchKernelGGL((k_forward_tiles<NM, J, JO, 2>), tgrid, dim3(256), tl, s, pl, theta,      \
+      hipLaunchKernelGGL((k_forward_tiles<NM, J, JO, 2>), tgrid, dim3(TW_THREADS), tl, s, pl, theta, \
                          omega, der, X, Y, y_cols, n, fo, logp, se, lse_m, lse_s, se_sum);         \
     } else {                                                                                       \
       set_lds_limit((const void*)k_forward_tiles<NM, J, JO, 1>, tl);                               \
-      hipLaunchKernelGGL((k_forward_tiles<NM, J, JO, 1>), tgrid, dim3(256), tl, s, pl, theta,      \
+      hipLaunchKernelGGL((k_forward_tiles<NM, J, JO, 1>), tgrid, dim3(TW_THREADS), tl, s, pl, theta, \
                          omega, der, X, Y, y_cols, n, fo, logp, se, lse_m, lse_s, se_sum);         \
     }                                                                                              \
   } while (0)
