@@ -90,6 +90,20 @@ def cpu_baseline(seconds):
             "note": "BLAS matmuls use the listed threads; numpy elementwise/trig is single-threaded"}
 
 
+def pmc_traffic(prefix):
+    """HBM-side bytes per launch of the kernels named `prefix...` (dispatch-weighted mean), from the
+    committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes (profiles/r01b/pmc_traffic.json, made by
+    scripts/gpu_profile_round.sh; FETCH doubled per MI355X_MICROARCH.md §HBM).  None if absent."""
+    path = os.path.join(ROOT, "profiles", "r01b", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as fh:
+        ks = json.load(fh)["kernels"]
+    sel = [v for k, v in ks.items() if k.startswith(prefix) and "dispatches" in v]
+    n = sum(v["dispatches"] for v in sel)
+    return round(sum(v["traffic"] * v["dispatches"] for v in sel) / n) if n else None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -197,7 +211,10 @@ def main():
     roof = {"kernel": dom, "bound": "mfma",
             "achieved": round(fl_dom / (ms_dom * 1e-3) / 1e12, 6),
             "peak": FP32_MFMA_PEAK / 1e12, "unit": "TFLOP/s",
-            "frac": round(fl_dom / (ms_dom * 1e-3) / FP32_MFMA_PEAK, 8), "traffic": None,
+            "frac": round(fl_dom / (ms_dom * 1e-3) / FP32_MFMA_PEAK, 8),
+            "traffic": pmc_traffic(dom),
+            "traffic_source": "profiles/r01b/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE "
+                              "passes of this bench; bytes per launch incl. Infinity-Cache hits)",
             "avg_launch_us": round(ms_dom * 1e3, 3),
             "flops_per_launch": int(fl_dom),
             "method": "hipEvent pair around the kernel minus an empty pair (dgprf_profile_step)",
@@ -214,7 +231,9 @@ def main():
                  "achieved": round(fp / (pred_kernel_ms * 1e-3) / 1e12, 4),
                  "peak": FP32_MFMA_PEAK / 1e12, "unit": "TFLOP/s",
                  "frac": round(fp / (pred_kernel_ms * 1e-3) / FP32_MFMA_PEAK, 5),
-                 "traffic": None, "avg_launch_us": round(pred_kernel_ms * 1e3, 2),
+                 "traffic": pmc_traffic("k_forward_tiles"),
+                 "algorithmic_bytes": int(4 * CFG["N_test"] * (CFG["D"] + 1 + 3 * 2)),
+                 "avg_launch_us": round(pred_kernel_ms * 1e3, 2),
                  "flops_per_launch": int(fp)}
 
     # ---------------- many chains per GPU (aggregate chain-steps/s; extra, not `value`)

@@ -5,6 +5,9 @@
 //   A: hipGraph of S steps x 7 kernels (grid 13x16 WGs of 256 threads, like the step kernels)
 //   B: one persistent kernel, G resident WGs, 7 phases per step separated by a counter barrier
 //      (agent release before arrive, relaxed polling with s_sleep, agent acquire after).
+//   C: like B, but the cross-workgroup data itself moves with agent-scope relaxed atomic loads /
+//      stores (coherent without L2 writeback / invalidate) and the barrier has no fences: stores
+//      drained with s_waitcnt vmcnt(0) before the arrive.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -79,6 +82,52 @@ __global__ __launch_bounds__(256) void k_persistent(float* buf, unsigned* ctr, u
   }
 }
 
+__device__ __forceinline__ void grid_sync_light(unsigned* ctr, unsigned target, unsigned* tmo) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned spins = 0;
+    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 24)) {
+        *tmo = 1;
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void k_persistent_light(float* buf, unsigned* ctr, unsigned* tmo,
+                                                          int steps, int work_blocks) {
+  const unsigned G = gridDim.x;
+  unsigned phase_no = 0;
+  for (int st = 0; st < steps; ++st) {
+    for (int ph = 0; ph < NPH; ++ph) {
+      float* src = buf + (size_t)(ph % 2) * SLOTS * 16;
+      float* dst = buf + (size_t)((ph + 1) % 2) * SLOTS * 16;
+      for (int wb = blockIdx.x; wb < work_blocks; wb += G) {
+        const int i = wb * blockDim.x + threadIdx.x;
+        float v[16];
+#pragma unroll
+        for (int s = 0; s < 16; ++s)
+          v[s] = __hip_atomic_load(src + ((i * 7 + s * 131) % SLOTS) * 16 + s, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        float a = 0.f;
+#pragma unroll
+        for (int s = 0; s < 16; ++s) a += v[s];
+        if ((i & 15) == 0)
+          __hip_atomic_store(dst + (i >> 4) % SLOTS * 16 + (i & 15), a * 0.5f + 1.f,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      ++phase_no;
+      grid_sync_light(ctr, phase_no * G, tmo);
+      if (__hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+    }
+  }
+}
+
 int main() {
   float* buf;
   unsigned *ctr, *tmo;
@@ -142,6 +191,29 @@ int main() {
       best = ms < best ? ms : best;
     }
     printf("B persistent G=%3d WGs : %.2f us/step  (%.2f us/phase)\n", G, best * 1e3 / S,
+           best * 1e3 / S / NPH);
+  }
+  // ---- C: persistent kernel, coherent data accesses, fence-free barrier
+  for (int G : {208, 64, 16}) {
+    float best = 1e30f;
+    for (int rep = 0; rep < 3; ++rep) {
+      CHECK(hipMemsetAsync(ctr, 0, 256, s));
+      CHECK(hipMemsetAsync(tmo, 0, 256, s));
+      CHECK(hipEventRecord(e0, s));
+      hipLaunchKernelGGL(k_persistent_light, dim3(G), dim3(256), 0, s, buf, ctr, tmo, S, 208);
+      CHECK(hipEventRecord(e1, s));
+      CHECK(hipEventSynchronize(e1));
+      float ms;
+      CHECK(hipEventElapsedTime(&ms, e0, e1));
+      unsigned h_tmo = 0;
+      CHECK(hipMemcpy(&h_tmo, tmo, 4, hipMemcpyDeviceToHost));
+      if (h_tmo) {
+        printf("C light G=%d: barrier timeout\n", G);
+        return 2;
+      }
+      best = ms < best ? ms : best;
+    }
+    printf("C light  G=%3d WGs : %.2f us/step  (%.2f us/phase)\n", G, best * 1e3 / S,
            best * 1e3 / S / NPH);
   }
   return 0;
