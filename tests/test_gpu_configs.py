@@ -1,0 +1,142 @@
+"""BASELINE.json configs 3-5 as parity cases: the full model shapes (layer kinds, n_rf, widths,
+likelihood) with batches / test sets small enough for the float64 oracle.
+
+  config 3: 3-layer ARC, n_rf=2048, g=[9,9,1], D=9 (protein-shaped), Gaussian
+  config 4: 4-layer RBF, n_rf=4096, g=[30,30,30,10], D=784 (MNIST-shaped), softmax
+  config 5: 5-layer [RBF,ARC,RBF,ARC,RBF], n_rf=8192, g=[16,16,16,16,1], D=16, Gaussian
+
+Tolerances (fp32 device vs float64 oracle): forward / log p 5e-5 of the output scale (1e-4 for the
+K = 8192-long contractions of config 4), W gradients 2e-4 of the gradient scale, one injected-noise
+SGHMC update 2e-5; per-row predictive log p 2e-5 of the log p scale (an untrained random model's
+log p reaches |log p| ~ 80 here, so an absolute 1e-4 would ask for 1e-6 relative).
+
+ARC layers' relu has a kink: an inner product A within fp32 rounding (~1e-6) of 0 may take either
+side in fp32 (device or numpy alike), flipping 1[A > 0] and one term of every gradient below that
+layer by c dPhi.  Gradient / update cases therefore use rows whose float64 A stays >= 1e-5 from 0
+in every ARC layer (`_rows_off_kinks`); the forward itself is continuous there and is not filtered.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import dgp_oracle as O
+from test_gpu_parity import cpu, dev, pack, rel_err, unpack  # noqa: F401
+
+pytestmark = pytest.mark.gpu
+
+CONFIGS = {
+    3: dict(kinds=["ARC"] * 3, n_rf=[2048] * 3, n_gp=[9, 9, 1], D=9, lik="gaussian", B=64,
+            n_test=500, ftol=5e-5),
+    4: dict(kinds=["RBF"] * 4, n_rf=[4096] * 4, n_gp=[30, 30, 30, 10], D=784, lik="softmax", B=32,
+            n_test=64, ftol=1e-4),
+    5: dict(kinds=["RBF", "ARC", "RBF", "ARC", "RBF"], n_rf=[8192] * 5, n_gp=[16, 16, 16, 16, 1],
+            D=16, lik="gaussian", B=48, n_test=300, ftol=5e-5),
+}
+
+
+def _model(c, seed):
+    from dgprf import engine as E
+    from likelihoods import Gaussian, Softmax
+    from models.dgp import DGP_RF
+    E.set_seed(seed)
+    d_out = c["n_gp"][-1]
+    m = DGP_RF(c["D"], d_out, n_hidden_layers=len(c["kinds"]), n_rf=c["n_rf"], n_gp=c["n_gp"],
+               likelihood=Gaussian(variance=0.1) if c["lik"] == "gaussian" else Softmax(),
+               kernel_type_list=c["kinds"])
+    p = O.Params(c["D"], d_out, c["n_rf"], c["n_gp"], c["kinds"], c["lik"], False,
+                 z=[cpu(m.BNN.layers[2 * l].z) for l in range(len(c["kinds"]))],
+                 W=[cpu(w) for w in m.W_mcmc],
+                 log_inv_ls=[cpu(k.log_inv_length_scale) for k in m.kernel_list],
+                 lik_log_var=np.log(0.1))
+    return m, p
+
+
+def _data(c, n, seed):
+    rng = np.random.default_rng(seed)
+    d_out = c["n_gp"][-1]
+    if c["lik"] == "softmax":
+        X = rng.uniform(-0.5, 0.5, (n, c["D"]))  # normalize_MNIST range
+        Y = rng.integers(0, d_out, (n, 1)).astype(float)
+    else:
+        X = rng.standard_normal((n, c["D"]))
+        Y = rng.standard_normal((n, d_out))
+    return X.astype(np.float32).astype(np.float64), Y.astype(np.float32).astype(np.float64)
+
+
+def _rows_off_kinks(c, p, X, Y, n, tau=1e-5):
+    """The first n rows whose ARC-layer inner products all satisfy |A| >= tau (float64 oracle)."""
+    _, cache = O.forward(p, X, keep=True)
+    ok = np.ones(X.shape[0], dtype=bool)
+    for l, k in enumerate(c["kinds"]):
+        if k == "ARC":
+            ok &= np.min(np.abs(cache[l][1]), axis=1) >= tau
+    idx = np.nonzero(ok)[0][:n]
+    assert len(idx) == n, "not enough rows away from the relu kink"
+    return X[idx], Y[idx]
+
+
+@pytest.mark.parametrize("cfg", [3, 4, 5])
+def test_config_forward_and_grad(dev, cfg):
+    c = CONFIGS[cfg]
+    m, p = _model(c, 10 + cfg)
+    X, Y = _data(c, 2 * c["B"], cfg)
+    X, Y = _rows_off_kinks(c, p, X, Y, c["B"])
+    F = cpu(m.BNN(X))
+    assert rel_err(F, O.forward(p, X)) < c["ftol"]
+    lp = cpu(m.log_likelihood(X, Y))
+    ref_lp = O.log_prob(p, O.forward(p, X), Y)
+    assert np.max(np.abs(lp - ref_lp)) < c["ftol"] * max(1.0, np.max(np.abs(ref_lp)))
+    N_ = 45_730 if cfg == 3 else (60_000 if cfg == 4 else 10_000_000)
+    G = unpack(m._engine, m._engine.grad(X, Y, N_))
+    ref = O.grad_W(p, X, Y, N_)
+    for l in range(len(c["kinds"])):
+        assert rel_err(G[l], ref[l]) < 2e-4, (cfg, l)
+
+
+@pytest.mark.parametrize("cfg", [3, 5])
+def test_config_sghmc_step_injected_noise(dev, cfg):
+    c = CONFIGS[cfg]
+    m, p = _model(c, 20 + cfg)
+    eng = m._engine
+    X, Y = _data(c, 2 * c["B"], 100 + cfg)
+    X, Y = _rows_off_kinks(c, p, X, Y, c["B"])
+    L = len(c["kinds"])
+    rng = np.random.default_rng(cfg)
+    m.precond_update(None, 1000, precond_type="identity")
+    m0 = [cpu(eng.mom_view(l)).astype(np.float64) for l in range(L)]
+    xi = [rng.standard_normal(w.shape) for w in p.W]
+    eng.step(X, Y, 1000, 0.01, 0.9, 1.0, xi=pack(eng, xi))
+    O.sgmcmc_step(p, m0, X, Y, 1000, 0.01, 0.9, 1.0, [1.0] * L, xi)
+    for l in range(L):
+        assert rel_err(cpu(eng.W_view(l)), p.W[l]) < 2e-5, (cfg, l)
+
+
+@pytest.mark.parametrize("cfg", [3, 4, 5])
+def test_config_predictive_rows(dev, cfg):
+    """eval_log_likelihood(_and_se) over a test set (tile kernel for configs 3 and 5, the general
+    row kernel for config 4's D = 784) against the oracle, row by row."""
+    c = CONFIGS[cfg]
+    m, p = _model(c, 30 + cfg)
+    Xt, Yt = _data(c, c["n_test"], 200 + cfg)
+    out = m._engine.forward(Xt, Yt, logp=True)
+    lp = cpu(out["logp"][0])
+    ref = O.log_prob(p, O.forward(p, Xt), Yt)
+    assert np.max(np.abs(lp - ref)) < 2e-5 * max(1.0, np.max(np.abs(ref)))
+
+
+@pytest.mark.parametrize("cfg", [3, 5])
+def test_config_graph_steps_finite_and_deterministic(dev, cfg):
+    """200 graph-replayed steps with on-device minibatches at the config's N (config 5 scaled to
+    N = 2e5 rows to bound memory in the test): finite, and bit-identical on replay."""
+    c = CONFIGS[cfg]
+    n = 45_730 if cfg == 3 else 200_000
+    X = torch.randn(n, c["D"], device=dev)
+    Y = torch.randn(n, 1, device=dev)
+    out = []
+    for _ in range(2):
+        m, _ = _model(c, 40 + cfg)
+        m.precond_update(None, n, precond_type="identity")
+        m.run_sgmcmc(X, Y, n, 200, batch_size=200, lr=0.01, momentum_decay=0.9)
+        out.append(m._engine.theta.clone())
+        assert torch.isfinite(out[-1]).all()
+    assert torch.equal(out[0], out[1])
