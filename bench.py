@@ -104,6 +104,69 @@ def pmc_traffic(prefix):
     return round(sum(v["traffic"] * v["dispatches"] for v in sel) / n) if n else None
 
 
+def bench_config(cfg, dev, rank, world, barrier_sync, max_over_ranks, steps):
+    """Steps/s and predictive samples/s of BASELINE config 3, 4 or 5 (dgprf.data.CONFIGS): the full
+    model shape on synthetic data of the config's size, one chain per GPU, graph-replayed steps."""
+    from dgprf import engine as E
+    from dgprf.data import CONFIGS, classification_data, regression_data
+    from dgprf.distributed import rank_seed
+    from dgprf.predictive import PredictiveLSE
+    from likelihoods import Gaussian, Softmax
+    from models.dgp import DGP_RF
+    c = CONFIGS[cfg]
+    n, nt = c["n"], c["n_test"]
+    if c["likelihood"] == "softmax":
+        X, Y = classification_data(n, c["d_in"], c["d_out"], seed=0, device=dev)
+        Xt, Yt = classification_data(nt, c["d_in"], c["d_out"], seed=1, device=dev)
+        lik = Softmax()
+    else:
+        X, Y, a = regression_data(n, c["d_in"], seed=0, device=dev)
+        Xt, Yt, _ = regression_data(nt, c["d_in"], seed=1, device=dev, a=a)
+        lik = Gaussian(variance=c["variance"])
+    E.set_seed(rank_seed(20 + cfg, rank))
+    m = DGP_RF(c["d_in"], c["d_out"], n_hidden_layers=len(c["kinds"]), n_rf=c["n_rf"],
+               n_gp=c["n_gp"], likelihood=lik, kernel_type_list=c["kinds"])
+    m.precond_update(None, n, precond_type="identity")
+    run = dict(batch_size=c["batch"], lr=c["lr"], momentum_decay=c["beta"], temperature=c["T"],
+               steps_per_graph=100, perm_seed=rank_seed(cfg, rank))
+    m.run_sgmcmc(X, Y, n, 100, **run)
+    barrier_sync()
+    t0 = time.perf_counter()
+    m.run_sgmcmc(X, Y, n, steps, **run)
+    barrier_sync()
+    t_s = max_over_ranks(time.perf_counter() - t0)
+    assert torch.isfinite(m._engine.theta).all(), f"config {cfg} chain diverged"
+    pl = m._engine.layout
+    L = len(c["kinds"])
+    d, R, P, g = list(pl.d[:L]), list(pl.n_rf[:L]), list(pl.P[:L]), list(pl.n_gp[:L])
+    fwd_f, bwd_f = step_flops(c["batch"], d, R, P, g)
+    acc = PredictiveLSE(m._engine, Xt, Yt)
+    acc.add_sample()
+    S = 3 if cfg == 5 else 10
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    barrier_sync()
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(S):
+        acc.add_sample(build=False)
+    ev1.record()
+    barrier_sync()
+    t_p = max_over_ranks(time.perf_counter() - t0)
+    k_ms = ev0.elapsed_time(ev1) / S
+    fp = pred_flops(nt, d, R, P, g)
+    out = {"workload": f"{L}-layer {'/'.join(c['kinds'])} n_rf={c['n_rf'][0]} g={c['n_gp']} "
+                       f"D={c['d_in']} N={n} B={c['batch']} {c['likelihood']}",
+           "steps_per_s": round(world * steps / t_s, 1),
+           "us_per_step": round(t_s * 1e6 / steps, 2),
+           "step_mflop": round((sum(fwd_f) + sum(bwd_f)) / 1e6, 2),
+           "predictive_samples_per_s": round(world * S / t_p, 3), "n_test": nt,
+           "predictive_kernel_ms": round(k_ms, 3),
+           "predictive_mfma_frac": round(fp / (k_ms * 1e-3) / FP32_MFMA_PEAK, 4)}
+    del m, acc, X, Y, Xt, Yt
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -116,6 +179,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-reps", type=int, default=200)
+    ap.add_argument("--other-configs", type=int, default=1)
+    ap.add_argument("--other-steps", type=int, default=1000)
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -279,6 +344,13 @@ def main():
                       "us_per_step": round(t_fb * 1e6 / k_fb, 3), "steps": k_fb,
                       "sampled": "W, log_amplitude, log_inv_length_scale (ARD), lik_log_var"}
 
+    # ---------------- BASELINE configs 3-5 at their full model shapes (extra, not `value`)
+    other = {}
+    if args.other_configs:
+        for cfg in (3, 4, 5):
+            other[f"config{cfg}"] = bench_config(cfg, dev, rank, world, barrier_sync,
+                                                 max_over_ranks, args.other_steps)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_seconds)
@@ -302,7 +374,8 @@ def main():
                            "test_loglik": round(ll, 6), "test_rmse": round(rmse, 6),
                            "ms_per_sample": round(t_pred * 1e3 / args.pred_samples, 4)},
             "roofline": roof, "roofline_predictive": roof_pred, "cpu_baseline": cpu,
-            "multi_chain": multi, "full_bayes": full_bayes, "device": torch.cuda.get_device_name(dev),
+            "multi_chain": multi, "full_bayes": full_bayes, "other_configs": other or None,
+            "device": torch.cuda.get_device_name(dev),
         }
         print(json.dumps(line), flush=True)
     if world > 1:

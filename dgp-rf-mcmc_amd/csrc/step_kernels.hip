@@ -64,6 +64,8 @@ struct LayerK {
   int32_t fast, fprev_off, dsrc_off, xmag, dmag;
   int32_t n_rt, ns, rt_per_xcd;  // XCD-aware block -> (row tile, slice) map
   // full_bayesian=True (k_step_bwd<..., FB = true>)
+  const float* a0;      // precomputed A_1 [align32(B)][R] (layer 0 with d > 32; chain stride
+                        // ws_cs), nullptr otherwise
   const float* z;       // z_l [d][R] (shared by the chains)
   float* hp;            // hyper partials [n_rt_pad][NSM][round4(2d+1)] of chain 0 (stride ws_cs)
   float* hpl;           // lik_log_var partials [n_rt_pad] (last layer)
@@ -365,9 +367,10 @@ __global__ __launch_bounds__(256) void k_step_fwd(const LayerK a) {
   DGPRF_STAMP(stamp_base, 1);
   if (a.fast) {
     elem_prologue(a, chain, row0, 0, xs, red, 0, red, red);  // no dF tile: unused targets
-  } else {
+  } else if (KS > 0 || !a.a0) {
     load_x_tile(a, chain, row0, xs);
   }
+  const float* a0 = KS == 0 && a.a0 ? a.a0 + (int64_t)chain * a.ws_cs + (int64_t)(row0 + lr) * R : nullptr;
   __syncthreads();
   DGPRF_STAMP(stamp_base, 2);
 
@@ -383,7 +386,8 @@ __global__ __launch_bounds__(256) void k_step_fwd(const LayerK a) {
   for (int i = 0; i < cpw; ++i) {
     const int f0 = chunk_f0(i);
     if (f0 >= R) break;
-    const f4 at = a_tile<KS, false>(om, R, d, f0, omk, xf, xs, a.xst, lr, lq);
+    const f4 at = (KS == 0 && a0) ? *reinterpret_cast<const f4*>(a0 + f0 + 4 * lq)
+                                  : a_tile<KS, false>(om, R, d, f0, omk, xf, xs, a.xst, lr, lq);
     float p0[4], p1[4];
     features<RBF>(at, cl, p0, p1);
     float wc[NOT][4][2];
@@ -556,7 +560,7 @@ __global__ __launch_bounds__(256) void k_step_bwd(const LayerK a) {
     DGPRF_STAMP(stamp_base, 4);
   } else {
     if (dphi) stage_load(fb0);
-    load_x_tile(a, chain, row0, xs);
+    if (KS > 0 || !a.a0 || FB) load_x_tile(a, chain, row0, xs);
     for (int e = threadIdx.x; e < TR * g; e += blockDim.x) {  // dF (or F_L) slice sums; Y alongside
       const int r = e / g, o = e - r * g, b = row0 + r, bc = min(b, B - 1);
       const float v = sum_slices((a.last ? fpl : dxn) + (int64_t)bc * g + o, (int64_t)B * g);
@@ -686,10 +690,20 @@ __global__ __launch_bounds__(256) void k_step_bwd(const LayerK a) {
       for (int dt = 0; dt < 4; ++dt)
         oxv[dt] = *reinterpret_cast<const f4*>(osl + (dt * 16 + lr) * OST + wave * 16 + 4 * lq);
     }
-    const f4 at_t = a_tile<KS, true>(om, R, d, f0, omk, xf, xs, a.xst, lr, lq);
+    // layer 0 with d > 32: both orientations read the precomputed A_1 (k_step_agemm)
+    const float* a0 = KS == 0 && a.a0 ? a.a0 + (int64_t)chain * a.ws_cs + (int64_t)row0 * R + f0
+                                      : nullptr;
+    f4 at_t;
+    if (KS == 0 && a0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) at_t[r] = a0[(int64_t)(4 * lq + r) * R + lr];
+    } else {
+      at_t = a_tile<KS, true>(om, R, d, f0, omk, xf, xs, a.xst, lr, lq);
+    }
     f4 at_n = f4zero(), dpc = f4zero(), dps = f4zero();
     if (dphi) {
-      at_n = a_tile<KS, false>(om, R, d, f0, omk, xf, xs, a.xst, lr, lq);
+      at_n = (KS == 0 && a0) ? *reinterpret_cast<const f4*>(a0 + (int64_t)lr * R + 4 * lq)
+                             : a_tile<KS, false>(om, R, d, f0, omk, xf, xs, a.xst, lr, lq);
       if (G1) {
         // g == 1: dPhi[b][f] = dF[b] W[f] (outer product, VALU)
 #pragma unroll
@@ -879,6 +893,32 @@ __device__ __forceinline__ void gather_row(const BatchDev& bd, int B, int d_in, 
   for (int k = 0; k < yb_cols; ++k) yd[k] = ys[k];
 }
 
+// Wide rows (d_in > GATHER_WIDE, e.g. 784 MNIST pixels): one 64-lane wave per row, lanes striding
+// over the columns (coalesced, all loads issued before the stores) instead of one thread per row.
+constexpr int GATHER_WIDE = 16;
+__device__ __forceinline__ void gather_row_wave(const BatchDev& bd, int B, int d_in, int yb_cols,
+                                                float* xb, float* yb, int chain, int64_t t, int b,
+                                                int lane) {
+  const int64_t row = batch_row(bd, B, chain, t, b);
+  const float* xs = bd.X + row * d_in;
+  float* xd = xb + (int64_t)b * d_in;
+  constexpr int U = 8;
+  for (int k0 = 0; k0 < d_in; k0 += 64 * U) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = k0 + 64 * u + lane;
+      v[u] = k < d_in ? xs[k] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = k0 + 64 * u + lane;
+      if (k < d_in) xd[k] = v[u];
+    }
+  }
+  for (int k = lane; k < yb_cols; k += 64) yb[(int64_t)b * yb_cols + k] = bd.Y[row * bd.y_cols + k];
+}
+
 struct GatherK {
   BatchDev bd;
   const int64_t* step;
@@ -890,9 +930,16 @@ struct GatherK {
 
 __global__ void k_gather(const GatherK a) {
   const int chain = blockIdx.y;
+  const int64_t t = *a.step + a.step_offset;
+  if (a.d_in > GATHER_WIDE) {  // one wave per row
+    const int b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (b < a.B)
+      gather_row_wave(a.bd, a.B, a.d_in, a.yb_cols, a.xb + (int64_t)chain * a.ws_cs,
+                      a.yb + (int64_t)chain * a.ws_cs, chain, t, b, threadIdx.x & 63);
+    return;
+  }
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= a.B) return;
-  const int64_t t = *a.step + a.step_offset;
   gather_row(a.bd, a.B, a.d_in, a.yb_cols, a.xb + (int64_t)chain * a.ws_cs,
              a.yb + (int64_t)chain * a.ws_cs, chain, t, b);
 }
@@ -1222,6 +1269,13 @@ __global__ __launch_bounds__(UPD_THREADS) void k_step_update(const UpdK a) {
   const int bx = (int)blockIdx.x - a.hyp_blocks;
   if (bx >= a.upd_blocks) {  // dedicated blocks: rows of step t+1 (off the path)
     const int64_t t = *a.step + (int64_t)a.step_offset;
+    if (a.d_in > GATHER_WIDE) {  // one-wave blocks: one row each
+      const int b = bx - a.upd_blocks;
+      if (a.gather_next && b < a.B)
+        gather_row_wave(a.bd, a.B, a.d_in, a.yb_cols, a.xb + (int64_t)chain * a.ws_cs,
+                        a.yb + (int64_t)chain * a.ws_cs, chain, t + 1, b, threadIdx.x);
+      return;
+    }
     const int b = (bx - a.upd_blocks) * UPD_THREADS + threadIdx.x;
     if (a.gather_next && b < a.B)
       gather_row(a.bd, a.B, a.d_in, a.yb_cols, a.xb + (int64_t)chain * a.ws_cs,
@@ -1309,6 +1363,90 @@ __global__ void k_advance(int64_t* step, int64_t by) {
 }
 
 // ------------------------------------------------------------------------- host helpers
+// ------------------------------------------------------------------------- wide first layer
+// A_1 = X Omega_1 for a first layer with d > 32 (BASELINE config 4: d = 784, R = 4096), written
+// to the workspace for the layer-0 forward and backward, which would otherwise each run a d-long
+// dependent k-step loop per 16-feature chunk.  One workgroup = 32 rows x 64 features; its 4 waves
+// own 16 x 32 sub-tiles (2 accumulators); K runs in LDS-staged blocks of 32 (X block [32][33],
+// Omega block [32][68]), the next block's loads in flight while the current one computes.  Rows
+// >= B and k >= d are staged as zeros.
+struct AgemmK {
+  const float* xrows;  // [B][d_in] of chain 0 (stride xrow_cs)
+  const float* om;     // Omega_1 [d][R] of chain 0 (stride om_cs)
+  float* aout;         // [align32(B)][R] of chain 0 (stride ws_cs)
+  int64_t xrow_cs, om_cs, ws_cs;
+  int32_t B, d, R, d_in;
+};
+constexpr int AG_KB = 32, AG_XST = 33, AG_OST = 68;
+
+__global__ __launch_bounds__(256) void k_step_agemm(const AgemmK a) {
+  __shared__ float xsm[2][32 * AG_XST];
+  __shared__ __attribute__((aligned(16))) float osm[2][AG_KB * AG_OST];
+  const int chain = blockIdx.z;
+  const int rb = blockIdx.y * 32, fb = blockIdx.x * 64;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lq = lane >> 4;
+  const int wr = wave >> 1, wc = wave & 1;
+  const float* X = a.xrows + (int64_t)chain * a.xrow_cs;
+  const float* om = a.om + (int64_t)chain * a.om_cs;
+  const int d = a.d, R = a.R;
+  // staging assignment: X block: 4 scalars per thread (row tid >> 3, k (tid & 7) * 4 + q);
+  // Omega block: 2 float4 per thread (k = e >> 4, features 4 (e & 15))
+  const int xr = tid >> 3, xk = (tid & 7) * 4;
+  const rsrc_t rx = make_rsrc(X, (int64_t)a.B * a.d_in);
+  const rsrc_t ro = make_rsrc(om, (int64_t)d * R);
+  float xv[4];
+  f4 ov[2];
+  auto load = [&](int kb) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = rb + xr, k = kb + xk + q;
+      xv[q] = bload1(rx, row < a.B && k < d ? (uint32_t)(((int64_t)row * a.d_in + k) * 4) : DGPRF_OOB);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int e = tid + 256 * j, k = kb + (e >> 4), f = fb + 4 * (e & 15);
+      ov[j] = bload4(ro, k < d && f < R ? (uint32_t)(((int64_t)k * R + f) * 4) : DGPRF_OOB);
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) xsm[buf][xr * AG_XST + xk + q] = xv[q];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int e = tid + 256 * j;
+      *reinterpret_cast<f4*>(&osm[buf][(e >> 4) * AG_OST + 4 * (e & 15)]) = ov[j];
+    }
+  };
+  f4 acc0 = f4zero(), acc1 = f4zero();
+  const int nkb = (d + AG_KB - 1) / AG_KB;
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int buf = kb & 1;
+    if (kb + 1 < nkb) load((kb + 1) * AG_KB);
+    const float* xb = &xsm[buf][(wr * 16 + lr) * AG_XST + lq];
+    const float* ob = &osm[buf][lq * AG_OST + wc * 32 + lr];
+#pragma unroll
+    for (int ks = 0; ks < AG_KB / 4; ++ks) {
+      const float xa = xb[4 * ks];
+      acc0 = mfma16(xa, ob[4 * ks * AG_OST], acc0);
+      acc1 = mfma16(xa, ob[4 * ks * AG_OST + 16], acc1);
+    }
+    if (kb + 1 < nkb) store(buf ^ 1);
+    __syncthreads();
+  }
+  // acc[r] = A[row wr*16 + 4lq + r][feature wc*32 + n*16 + lr]
+  float* out = a.aout + (int64_t)chain * a.ws_cs;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int64_t row = rb + wr * 16 + 4 * lq + r;
+    const int f = fb + wc * 32 + lr;
+    if (f < R) out[row * R + f] = acc0[r];
+    if (f + 16 < R) out[row * R + f + 16] = acc1[r];
+  }
+}
+
 LayerK make_layer_k(const dgprf_plan_t& pl, const StepDev& sd, int l, int& lds_floats) {
   LayerK a;
   const bool direct = sd.bd.mode == DGPRF_BATCH_DIRECT;
@@ -1356,6 +1494,7 @@ LayerK make_layer_k(const dgprf_plan_t& pl, const StepDev& sd, int l, int& lds_f
   a.ns = pl.ns[l];
   a.rt_per_xcd = (pl.n_row_tiles + 7) / 8;
   // full_bayesian=True: z rows, hyper partials, per-wave LDS sums [4][round4(2d+1)]
+  a.a0 = (l == 0 && pl.a0_off >= 0 && sd.ws) ? sd.ws + pl.a0_off : nullptr;
   a.z = sd.z ? sd.z + pl.omega_off[l] : nullptr;
   a.hp = sd.ws + pl.hpp_off[l];
   a.hpl = sd.ws + pl.hpl_off;
@@ -1455,6 +1594,21 @@ namespace dgprf {
 hipError_t launch_step_fwd(const dgprf_plan_t& pl, const StepDev& sd, int layer, hipStream_t s) {
   int lds_floats = 0;
   const LayerK a = make_layer_k(pl, sd, layer, lds_floats);
+  if (a.a0) {  // wide first layer: A_1 = X Omega_1 first (k_step_agemm)
+    AgemmK g;
+    g.xrows = a.xrows;
+    g.om = a.om;
+    g.aout = sd.ws + pl.a0_off;
+    g.xrow_cs = a.xrow_cs;
+    g.om_cs = a.om_cs;
+    g.ws_cs = pl.ws_chain;
+    g.B = pl.batch;
+    g.d = pl.d[0];
+    g.R = pl.n_rf[0];
+    g.d_in = pl.d_in;
+    dim3 ggrid((unsigned)((g.R + 63) / 64), (unsigned)((g.B + 31) / 32), pl.n_chains);
+    hipLaunchKernelGGL(k_step_agemm, ggrid, dim3(256), 0, s, g);
+  }
   dim3 grid(8 * a.rt_per_xcd * a.ns, 1, pl.n_chains);
   k_step_fwd_launch(pl.d[layer], pl.n_gp[layer], pl.kind[layer] == DGPRF_RBF, grid,
                     (size_t)lds_floats * sizeof(float), s, a);
@@ -1554,8 +1708,9 @@ hipError_t launch_step_update(const dgprf_plan_t& pl, const StepDev& sd, const U
     a.hyp_blocks = k.n_blocks;
     lds = (size_t)(5 * hsmax + max(4 * UPD_THREADS, hsmax) + UPD_THREADS + 4) * sizeof(float);
   }
-  const int64_t blocks = a.hyp_blocks + a.upd_blocks +
-                         (a.gather_next ? (pl.batch + UPD_THREADS - 1) / UPD_THREADS : 0);
+  const int64_t gblocks = !a.gather_next ? 0 : (pl.d_in > GATHER_WIDE ? pl.batch
+                                                    : (pl.batch + UPD_THREADS - 1) / UPD_THREADS);
+  const int64_t blocks = a.hyp_blocks + a.upd_blocks + gblocks;
   dim3 grid((unsigned)blocks, pl.n_chains);
   const bool xi = ud.xi != nullptr || ud.xi_resample != nullptr ||
                   (fb && (ud.xi_hyp != nullptr || ud.xi_hyp_resample != nullptr));
@@ -1592,7 +1747,8 @@ hipError_t launch_gather(const dgprf_plan_t& pl, const StepDev& sd, hipStream_t 
   a.d_in = pl.d_in;
   a.yb_cols = pl.yb_cols;
   a.step_offset = sd.step_offset;
-  dim3 grid((unsigned)((pl.batch + 255) / 256), pl.n_chains);
+  const int rows_per_block = pl.d_in > GATHER_WIDE ? 4 : 256;
+  dim3 grid((unsigned)((pl.batch + rows_per_block - 1) / rows_per_block), pl.n_chains);
   hipLaunchKernelGGL(k_gather, grid, dim3(256), 0, s, a);
   return hipGetLastError();
 }

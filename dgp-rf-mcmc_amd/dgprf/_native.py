@@ -22,7 +22,7 @@ RNG_NOISE, RNG_RESAMPLE, RNG_Z, RNG_W, RNG_MOMENTS = 1, 2, 3, 4, 5
 RNG_HYPER, RNG_HYPER_RESAMPLE = 6, 7
 HYP_KERNEL, HYP_LIK, HYP_MEAN = 1, 2, 4
 HMASS = 32  # hmass slots: log_amp l -> l, log_inv_ls l -> 8 + l, mean l -> 16 + l, lik_log_var -> 24
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 E_ARG, E_SHAPE, E_HIP, E_PLAN = -1, -2, -3, -4
 
@@ -50,7 +50,7 @@ class Plan(ctypes.Structure):
         ("omega_total", _i64), ("w_total", _i64), ("hyp_total", _i64), ("der_total", _i64),
         ("ws_chain", _i64), ("ws_total", _i64), ("hpp_off", _i64 * _L), ("hpl_off", _i64),
         ("xb_off", _i64), ("yb_off", _i64),
-        ("yb_cols", _i32), ("pad2", _i32),
+        ("yb_cols", _i32), ("pad2", _i32), ("a0_off", _i64),
     ]
 
 

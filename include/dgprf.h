@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define DGPRF_ABI_VERSION 2
+#define DGPRF_ABI_VERSION 3
 
 #define DGPRF_MAX_LAYERS 8
 #define DGPRF_MAX_G 64        /* max latent GPs per layer (n_gp[l]) */
@@ -138,6 +138,9 @@ typedef struct dgprf_plan {
   int64_t yb_off;                    /* gathered minibatch targets [B][yb_cols] (per chain)    */
   int32_t yb_cols;                   /* g_L (Gaussian) or 1 (softmax label)                    */
   int32_t pad2;
+  int64_t a0_off;                    /* layer 1 with d > 32 (e.g. the 784-wide MNIST input):
+                                        A_1 = X Omega_1 [align32(B)][R_1] precomputed by one tiled
+                                        MFMA GEMM per step (per chain); -1 when not used          */
 } dgprf_plan_t;
 
 /* Device state of the chains.  Replaces the tf.Variables W and their ad-hoc attributes
