@@ -41,9 +41,10 @@ struct UpdateDev {
 #ifdef DGPRF_STAMPS
 extern __device__ unsigned long long g_dgprf_stamps[];
 #define DGPRF_STAMP_SLOTS 16
+#define DGPRF_STAMP_BASES (17 * 4096)
 #define DGPRF_STAMP(base, i)                                                      \
   do {                                                                           \
-    if (threadIdx.x == 0) {                                                      \
+    if (threadIdx.x == 0 && (size_t)(base) < DGPRF_STAMP_BASES) {                \
       __builtin_amdgcn_sched_barrier(0);                                         \
       g_dgprf_stamps[(size_t)(base) * DGPRF_STAMP_SLOTS + (i)] =                 \
           __builtin_amdgcn_s_memtime();                                          \
@@ -59,7 +60,8 @@ extern __device__ unsigned long long g_dgprf_stamps[];
 // per-wave placement: slots 8..11 = HW_ID | XCC_ID << 32 of waves 0..3
 #define DGPRF_STAMP_HWID(base)                                                   \
   do {                                                                           \
-    if ((threadIdx.x & 63) == 0 && threadIdx.x < 256) {                          \
+    if ((threadIdx.x & 63) == 0 && threadIdx.x < 256 &&                          \
+        (size_t)(base) < DGPRF_STAMP_BASES) {                                    \
       const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);  \
       const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20);\
       g_dgprf_stamps[(size_t)(base) * DGPRF_STAMP_SLOTS + 8 + (threadIdx.x >> 6)] = \

@@ -22,8 +22,14 @@ from models.regression_model import RegressionDGP  # noqa: E402
 
 SLOTS = 16
 dev = torch.device("cuda", 0)
-X, Y, _ = regression_data(1_000_000, 8, 0, device=dev)
-m = RegressionDGP(8, 1, n_hidden_layers=3, n_rf=1024, n_gp=[8, 8, 1], likelihood=Gaussian())
+CFG = 5 if "--config5" in sys.argv else 2  # config 5: L=5 mixed RBF/ARC, n_rf=8192, g=16
+if CFG == 5:
+    X, Y, _ = regression_data(1_000_000, 16, 0, device=dev)
+    m = RegressionDGP(16, 1, n_hidden_layers=5, n_rf=8192, n_gp=[16, 16, 16, 16, 1],
+                      likelihood=Gaussian(), kernel_type_list=["RBF", "ARC", "RBF", "ARC", "RBF"])
+else:
+    X, Y, _ = regression_data(1_000_000, 8, 0, device=dev)
+    m = RegressionDGP(8, 1, n_hidden_layers=3, n_rf=1024, n_gp=[8, 8, 1], likelihood=Gaussian())
 FB = "--full-bayes" in sys.argv  # full_bayesian=True steps; hyper workgroups reported apart
 m.precond_update(None, 1_000_000, precond_type="identity", full_bayesian=FB)
 eng = m._engine
@@ -39,8 +45,11 @@ n = 17 * 4096 * SLOTS
 buf = (ctypes.c_ulonglong * n)()
 assert lib.dgprf_debug_read_stamps(buf, n) == 0
 S = np.frombuffer(buf, dtype=np.uint64).reshape(17, 4096, SLOTS).astype(np.int64)
-names = {0: "fwd0", 2: "fwd1", 4: "fwd2", 1: "bwd0", 3: "bwd1", 5: "bwd2", 16: "update"}
-order = [0, 2, 4, 5, 3, 1, 16]
+Lm = m.n_hidden_layers
+names = {2 * l: f"fwd{l}" for l in range(Lm)}
+names.update({2 * l + 1: f"bwd{l}" for l in range(Lm)})
+names[16] = "update"
+order = [2 * l for l in range(Lm)] + [2 * l + 1 for l in reversed(range(Lm))] + [16]
 if FB:  # the update kernel's first workgroups are the hyper ones (one per 1024 Omega elements + 1)
     pl = eng.layout
     n_hyp = sum((pl.d[l] * pl.n_rf[l] + 1023) // 1024 for l in range(eng.L)) + 1
