@@ -343,6 +343,15 @@ __device__ __forceinline__ bool w_ok(int ot, int r, int R, int g, int f0, int lr
 
 // ------------------------------------------------------------------------- forward
 template <int KS, int NOT, bool RBF, bool G1>
+// Minimum waves per SIMD the register allocation must allow.  Single-chain steps run one workgroup
+// per CU either way; with C chains per launch (13 x 16 x C workgroups) residency sets throughput:
+// the g <= 16, d <= 8 W-only backward at <= 168 VGPRs (3 waves/SIMD) measured 127k -> 156k
+// chain-steps/s at C = 64 and single-chain 36.3k -> 36.7k steps/s (config 3's ARC layers +3 %);
+// the wider / full-Bayes instances keep their registers (they would spill 20-200 VGPRs; config 5's
+// RBF d = 16 layers lost 8 % with 22 spilled).
+#ifndef DGPRF_STEP_WPE
+#define DGPRF_STEP_WPE 3
+#endif
 __global__ __launch_bounds__(256) void k_step_fwd(const LayerK a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   int rt, sl;
@@ -454,7 +463,7 @@ __global__ __launch_bounds__(256) void k_step_fwd(const LayerK a) {
 
 // ------------------------------------------------------------------------- backward
 template <int KS, int NOT, bool RBF, bool G1, bool FB>
-__global__ __launch_bounds__(256) void k_step_bwd(const LayerK a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NOT == 1 && !FB && (KS == 1 || KS == 2 || (KS == 4 && !RBF))) ? DGPRF_STEP_WPE : 1))) void k_step_bwd(const LayerK a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   int rt, sl;
   if (!tile_of_block(a, rt, sl)) return;
