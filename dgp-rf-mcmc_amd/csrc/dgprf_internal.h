@@ -93,6 +93,9 @@ hipError_t launch_step_update(const dgprf_plan_t& pl, const StepDev& sd, const U
 
 // minibatch rows of step *step + step_offset into the workspace (no-op for DGPRF_BATCH_DIRECT)
 hipError_t launch_gather(const dgprf_plan_t& pl, const StepDev& sd, hipStream_t s);
+// A = X Omega for n rows (X row stride ld, K = d), written [align32(n)][R]: the wide-first-layer GEMM
+hipError_t launch_agemm(const float* X, int64_t n, int ld, int d, const float* om, int R,
+                        float* aout, hipStream_t s);
 hipError_t launch_advance(int64_t* step, int64_t by, hipStream_t s);
 
 hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const float* omega,

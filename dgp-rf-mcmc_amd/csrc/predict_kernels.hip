@@ -11,6 +11,7 @@
 // Geometry: one workgroup = one 16-row tile walking ALL layers; its 4 waves split each layer's RF
 // features (16-feature chunks on v_mfma_f32_16x16x4_f32) and sum their F partials in LDS, so the
 // layer outputs never leave LDS and no cross-workgroup reduction exists.
+#include <algorithm>
 #include <cstdlib>
 
 #include "dgprf_internal.h"
@@ -55,7 +56,8 @@ template <bool SMALLD, int NOT, bool RBF, bool G1>
 __device__ __forceinline__ void layer_partial(const float* __restrict__ om,
                                               const float* __restrict__ W, int R, int d, int g,
                                               float cl, const float* xs, int xst, float* red,
-                                              int wave, int lr, int lq) {
+                                              int wave, int lr, int lq,
+                                              const float* __restrict__ arow = nullptr) {
   float xf[8];
 #pragma unroll
   for (int ks = 0; ks < 8; ++ks) xf[ks] = (SMALLD && 4 * ks < d) ? xs[lr * xst + 4 * ks + lq] : 0.f;
@@ -93,6 +95,8 @@ __device__ __forceinline__ void layer_partial(const float* __restrict__ om,
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks)
         if (4 * ks < d) at = mfma16(omk[ks], xf[ks], at);
+    } else if (arow) {  // precomputed A row (wide first layer): A[row lr][f0 + 4lq + r]
+      at = *reinterpret_cast<const f4*>(arow + f0 + 4 * lq);
     } else {
       const int fa = f0 + lr;
       const int KS = round4(d) >> 2;
@@ -163,14 +167,17 @@ __global__ __launch_bounds__(256) void k_forward_rows(
     const float* __restrict__ der, const float* __restrict__ X, const float* __restrict__ Y,
     const int y_cols, const int64_t n, const FOut fo, float* __restrict__ logp_out,
     float* __restrict__ se_out, float* __restrict__ lse_m, float* __restrict__ lse_s,
-    float* __restrict__ se_sum) {
+    float* __restrict__ se_sum, const float* __restrict__ a0, const int64_t row_begin,
+    const int64_t row_end) {
+  // rows [row_begin, row_end) of the n-row set; a0 = A_1 = X Omega_1 of those rows
+  // ([row - row_begin][R_1], k_step_agemm) for a wide first layer, or nullptr
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const FwdLds LD = fwd_lds(pl);
   const int chain = blockIdx.y;
   const int64_t ochain = pl.hyp_per_chain ? (int64_t)chain * pl.omega_total : 0;
   const int64_t dchain = pl.hyp_per_chain ? (int64_t)chain * pl.der_total : 0;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, lr = lane & 15, lq = lane >> 4;
-  const int64_t row0 = (int64_t)blockIdx.x * TR;
+  const int64_t row0 = row_begin + (int64_t)blockIdx.x * TR;
   float* xs = smem;
   float* red = smem + LD.red_off;
   float* ft = smem + LD.ft_off;
@@ -181,11 +188,12 @@ __global__ __launch_bounds__(256) void k_forward_rows(
     const int d = pl.d[layer], dpad = round4(d);
     const int R = pl.n_rf[layer], g = pl.n_gp[layer];
     const int gp = layer > 0 ? pl.n_gp[layer - 1] : 0;
-    for (int e = threadIdx.x; e < TR * dpad; e += blockDim.x) {
+    const float* arow = (layer == 0 && a0) ? a0 + (row0 - row_begin + lr) * (int64_t)R : nullptr;
+    for (int e = threadIdx.x; !arow && e < TR * dpad; e += blockDim.x) {
       const int r = e / dpad, k = e - r * dpad;
       const int64_t b = row0 + r;
       float v = 0.f;
-      if (b < n && k < d) v = (k < gp) ? ft[r * LD.ftst + k] : X[b * pl.d_in + (k - gp)];
+      if (b < row_end && k < d) v = (k < gp) ? ft[r * LD.ftst + k] : X[b * pl.d_in + (k - gp)];
       xs[r * LD.xst + k] = v;
     }
     __syncthreads();
@@ -196,23 +204,33 @@ __global__ __launch_bounds__(256) void k_forward_rows(
       const float cl = der[dchain + layer];
       const int NOT = (g + 15) >> 4;
       const bool rbf = pl.kind[layer] == DGPRF_RBF;
-      // runtime (layer) -> compile-time body: output tiles, kernel kind, g == 1 VALU path
-      if (g == 1) {
-        if (rbf) layer_partial<SMALLD, 1, true, true>(om, W, R, d, g, cl, xs, LD.xst, red, wave, lr, lq);
-        else layer_partial<SMALLD, 1, false, true>(om, W, R, d, g, cl, xs, LD.xst, red, wave, lr, lq);
-      } else if (NOT == 1) {
-        if (rbf) layer_partial<SMALLD, 1, true, false>(om, W, R, d, g, cl, xs, LD.xst, red, wave, lr, lq);
-        else layer_partial<SMALLD, 1, false, false>(om, W, R, d, g, cl, xs, LD.xst, red, wave, lr, lq);
-      } else if (NOTMAX >= 2 && NOT == 2) {
-        if (rbf) layer_partial<SMALLD, (NOTMAX >= 2 ? 2 : 1), true, false>(om, W, R, d, g, cl, xs, LD.xst, red, wave, lr, lq);
-        else layer_partial<SMALLD, (NOTMAX >= 2 ? 2 : 1), false, false>(om, W, R, d, g, cl, xs, LD.xst, red, wave, lr, lq);
-      } else if (NOTMAX >= 3 && NOT == 3) {
-        if (rbf) layer_partial<SMALLD, (NOTMAX >= 3 ? 3 : 1), true, false>(om, W, R, d, g, cl, xs, LD.xst, red, wave, lr, lq);
-        else layer_partial<SMALLD, (NOTMAX >= 3 ? 3 : 1), false, false>(om, W, R, d, g, cl, xs, LD.xst, red, wave, lr, lq);
-      } else if (NOTMAX >= 4) {
-        if (rbf) layer_partial<SMALLD, (NOTMAX >= 4 ? 4 : 1), true, false>(om, W, R, d, g, cl, xs, LD.xst, red, wave, lr, lq);
-        else layer_partial<SMALLD, (NOTMAX >= 4 ? 4 : 1), false, false>(om, W, R, d, g, cl, xs, LD.xst, red, wave, lr, lq);
-      }
+      // runtime (layer) -> compile-time body: output tiles, kernel kind, g == 1 VALU path; layers
+      // with d <= 32 take the register-fragment path even when another layer is wide
+#define DGPRF_LP(SD, NT, RB, G1_) \
+  layer_partial<SD, NT, RB, G1_>(om, W, R, d, g, cl, xs, LD.xst, red, wave, lr, lq, arow)
+#define DGPRF_LP_ALL(SD)                                                                        \
+  do {                                                                                          \
+    if (g == 1) {                                                                               \
+      if (rbf) DGPRF_LP(SD, 1, true, true);                                                     \
+      else DGPRF_LP(SD, 1, false, true);                                                        \
+    } else if (NOT == 1) {                                                                      \
+      if (rbf) DGPRF_LP(SD, 1, true, false);                                                    \
+      else DGPRF_LP(SD, 1, false, false);                                                       \
+    } else if (NOTMAX >= 2 && NOT == 2) {                                                       \
+      if (rbf) DGPRF_LP(SD, (NOTMAX >= 2 ? 2 : 1), true, false);                                \
+      else DGPRF_LP(SD, (NOTMAX >= 2 ? 2 : 1), false, false);                                   \
+    } else if (NOTMAX >= 3 && NOT == 3) {                                                       \
+      if (rbf) DGPRF_LP(SD, (NOTMAX >= 3 ? 3 : 1), true, false);                                \
+      else DGPRF_LP(SD, (NOTMAX >= 3 ? 3 : 1), false, false);                                   \
+    } else if (NOTMAX >= 4) {                                                                   \
+      if (rbf) DGPRF_LP(SD, (NOTMAX >= 4 ? 4 : 1), true, false);                                \
+      else DGPRF_LP(SD, (NOTMAX >= 4 ? 4 : 1), false, false);                                   \
+    }                                                                                           \
+  } while (0)
+      if (SMALLD || d <= 32) DGPRF_LP_ALL(true);
+      else DGPRF_LP_ALL(false);
+#undef DGPRF_LP_ALL
+#undef DGPRF_LP
     }
     const int GP = ((g + 15) >> 4) * 16;
     __syncthreads();
@@ -224,7 +242,7 @@ __global__ __launch_bounds__(256) void k_forward_rows(
       for (int w = 1; w < NW; ++w) v += red[w * TR * GP + r * GP + o];
       ft[r * LD.ftst + o] = v;
       const int64_t b = row0 + r;
-      if (out && b < n) out[b * g + o] = v;
+      if (out && b < row_end) out[b * g + o] = v;
     }
     __syncthreads();
   }
@@ -233,7 +251,7 @@ __global__ __launch_bounds__(256) void k_forward_rows(
   const bool want_lik = logp_out || se_out || lse_m;
   if (want_lik && threadIdx.x < TR) {
     const int64_t b = row0 + threadIdx.x;
-    if (b < n) {
+    if (b < row_end) {
       const int g = pl.n_gp[L - 1];
       const float* f = ft + threadIdx.x * LD.ftst;
       const float* y = Y + b * y_cols;
@@ -430,7 +448,8 @@ struct TileLds {
   int obuf, wbuf, o_off, w_off, xin_off, xin_st, f_off, ftst, total;
 };
 
-__host__ __device__ inline TileLds tile_lds(const dgprf_plan_t& pl, int notmax, int njo, int tpw) {
+__host__ __device__ inline TileLds tile_lds(const dgprf_plan_t& pl, int notmax, int njo, int tpw,
+                                            bool wide0 = false) {
   int gmax = 1;
   for (int l = 0; l < pl.n_layers; ++l) gmax = pl.n_gp[l] > gmax ? pl.n_gp[l] : gmax;
   TileLds T;
@@ -438,7 +457,7 @@ __host__ __device__ inline TileLds tile_lds(const dgprf_plan_t& pl, int notmax, 
   T.wbuf = 2 * 64 * tw_wst(notmax);         // [cos|sin][64 features][16 NOT + 4]
   T.o_off = 0;
   T.w_off = 2 * T.obuf;
-  T.xin_st = round4(pl.d_in);
+  T.xin_st = wide0 ? 4 : round4(pl.d_in);  // wide0: layer 0 reads A_1, no input rows staged
   T.xin_off = T.w_off + 2 * T.wbuf;
   T.ftst = gmax + 1;
   T.f_off = T.xin_off + TWW * tpw * TR * T.xin_st;
@@ -458,7 +477,10 @@ __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
                                            const float* __restrict__ W,
                                            const float* __restrict__ om, float cl,
                                            const TileLds& T, float* smem, float* xin, float* ftw,
-                                           int lr, int lq, int64_t wrow0, int64_t n, float* fout) {
+                                           int lr, int lq, int64_t wrow0, int64_t n, float* fout,
+                                           const float* __restrict__ arow0 = nullptr) {
+  // arow0 (wide first layer): A_1 rows of this wave's tiles, [row][R] (k_step_agemm); the Omega
+  // staging and A-tile MFMAs are skipped and A is read straight into the accumulator layout
   // G8 (2 <= g <= 8): W rows of 8 with the columns interleaved as 2 (o & 3) + (o >> 2), so a lane's
   // two 4x4-block operands (o = i, 4 + i) are one ds_read_b64
   constexpr int WST = G8 ? 8 : tw_wst(NOT);
@@ -497,7 +519,8 @@ __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
 #pragma unroll
     for (int j = 0; j < JO; ++j) {
       const int i = tid + 256 * j, k = i >> 4, c4 = i & 15;
-      so[j] = bload4(ro, k < d && fb + 4 * c4 < R ? (uint32_t)((k * R + fb + 4 * c4) * 4) : DGPRF_OOB);
+      so[j] = bload4(ro, !arow0 && k < d && fb + 4 * c4 < R ? (uint32_t)((k * R + fb + 4 * c4) * 4)
+                                                           : DGPRF_OOB);
     }
   };
   auto stage_store = [&](int buf, int fb) {
@@ -569,7 +592,7 @@ __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
     // APHASE: the four chunks' A tiles are issued together first (independent MFMA chains, so their
     // dependent latency overlaps), and the trig + F contraction of chunk c follows.
     f4 atc[APHASE ? 4 : 1][TPW];
-    if (APHASE) {
+    if (APHASE && !arow0) {
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         float om[KS];
@@ -586,7 +609,14 @@ __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       f4 at[TPW];
-      if (APHASE) {
+      if (arow0) {
+        // A_1 is in radians; the staged-Omega path computes it in revolutions (Omega x 1/2pi)
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+          at[t] = *reinterpret_cast<const f4*>(arow0 + (int64_t)(t * TR + lr) * R + fb + 16 * c + 4 * lq);
+          if (REV) at[t] = at[t] * 0.15915494309189535f;
+        }
+      } else if (APHASE) {
 #pragma unroll
         for (int t = 0; t < TPW; ++t) at[t] = atc[c][t];
       } else {
@@ -757,21 +787,28 @@ __device__ unsigned long long g_pred_stamps[1 << 20];
   } while (0)
 #endif
 
-template <int NOTMAX, int JW, int JO, int TPW>
-__global__ __launch_bounds__(TW_THREADS) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? DGPRF_TILE_WAVES : 2)))
+// WIDE: layer 0 reads a precomputed A_1 (separate instantiations keep the common kernels' registers);
+// g > 16 instances (NOTMAX > 1) are budgeted for 2 waves/SIMD: at 4 they spilled ~300 VGPRs.
+template <int NOTMAX, int JW, int JO, int TPW, bool WIDE>
+__global__ __launch_bounds__(TW_THREADS)
+__attribute__((amdgpu_waves_per_eu((TPW == 1 && NOTMAX == 1) ? DGPRF_TILE_WAVES : 2)))
 void k_forward_tiles(
     const dgprf_plan_t pl, const float* __restrict__ theta, const float* __restrict__ omega,
     const float* __restrict__ der, const float* __restrict__ X, const float* __restrict__ Y,
     const int y_cols, const int64_t n, const FOut fo, float* __restrict__ logp_out,
     float* __restrict__ se_out, float* __restrict__ lse_m, float* __restrict__ lse_s,
-    float* __restrict__ se_sum) {
+    float* __restrict__ se_sum, const float* __restrict__ a0, const int64_t row_begin_,
+    const int64_t row_end_) {
+  // rows [row_begin, row_end) of the n-row set; a0 = A_1 of those rows for a wide first layer
+  // (the other instantiations always cover all n rows in one launch: constants, no extra registers)
+  const int64_t row_begin = WIDE ? row_begin_ : 0, row_end = WIDE ? row_end_ : n;
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const TileLds T = tile_lds(pl, NOTMAX, JO, TPW);
+  const TileLds T = tile_lds(pl, NOTMAX, JO, TPW, WIDE);
   const int chain = blockIdx.y;
   const int64_t ochain = pl.hyp_per_chain ? (int64_t)chain * pl.omega_total : 0;
   const int64_t dchain = pl.hyp_per_chain ? (int64_t)chain * pl.der_total : 0;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, lr = lane & 15, lq = lane >> 4;
-  const int64_t wrow0 = (int64_t)blockIdx.x * TW_ROWS * TPW + wave * TR * TPW;
+  const int64_t wrow0 = row_begin + (int64_t)blockIdx.x * TW_ROWS * TPW + wave * TR * TPW;
   float* xin = smem + T.xin_off + wave * TPW * TR * T.xin_st;
   float* ftw = smem + T.f_off + wave * round4(TPW * TR * T.ftst);
   const float* Wc = theta + (int64_t)chain * pl.w_total;
@@ -784,7 +821,7 @@ void k_forward_tiles(
   for (int e = lane; e < TPW * TR * T.xin_st; e += 64) {
     const int r = e / T.xin_st, k = e - r * T.xin_st;
     const int64_t b = wrow0 + r;
-    xin[e] = (b < n && k < pl.d_in) ? X[b * pl.d_in + k] : 0.f;
+    xin[e] = (!WIDE && b < row_end && k < pl.d_in) ? X[b * pl.d_in + k] : 0.f;
   }
   for (int e = lane; e < TPW * TR * T.ftst; e += 64) ftw[e] = 0.f;
   __syncthreads();
@@ -793,16 +830,17 @@ void k_forward_tiles(
     const float* __restrict__ W = Wc + pl.w_off[layer];
     const float cl = der[dchain + layer];
     const int g = pl.n_gp[layer], NOT = (g + 15) >> 4;
-    const bool rbf = pl.kind[layer] == DGPRF_RBF, ks2 = pl.d[layer] <= 8;
+    const float* arow0 = (WIDE && layer == 0) ? a0 + (wrow0 - row_begin) * (int64_t)pl.n_rf[0] : nullptr;
+    const bool rbf = pl.kind[layer] == DGPRF_RBF, ks2 = pl.d[layer] <= 8 || arow0;
     float* fout = fo.p[layer] ? fo.p[layer] + (int64_t)chain * n * g : nullptr;
 #define DGPRF_TL(NT, RB, G1_, G8_)                                                                     \
   do {                                                                                              \
     if (ks2)                                                                                        \
       tile_layer<NT, RB, G1_, G8_, JW, JO, 2, TPW>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, \
-                                              n, fout);                                             \
+                                              row_end, fout, arow0);                                \
     else                                                                                            \
       tile_layer<NT, RB, G1_, G8_, JW, JO, 4 * JO, TPW>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq,  \
-                                                   wrow0, n, fout);                                 \
+                                                   wrow0, row_end, fout);                           \
   } while (0)
     if (g == 1) {
       if (rbf) DGPRF_TL(1, true, true, false);
@@ -827,7 +865,7 @@ void k_forward_tiles(
   const bool want_lik = logp_out || se_out || lse_m;
   for (int t = 0; t < TPW; ++t) {
     const int64_t b = wrow0 + t * TR + lr;
-    if (want_lik && lq == 0 && b < n) {
+    if (want_lik && lq == 0 && b < row_end) {
       const int g = pl.n_gp[L - 1];
       const float* f = ftw + (t * TR + lr) * T.ftst;
       const float* y = Y + b * y_cols;
@@ -889,72 +927,106 @@ hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const
     smalld = smalld && pl.d[l] <= 32;
     notmax = max(notmax, (pl.n_gp[l] + 15) >> 4);
   }
-  // tile kernel: d <= 32, g <= 64, R % 4 == 0 in every layer, d_in <= 32
-  bool tiles = pl.d_in <= 32;
+  // wide first layer (d_1 > 32, e.g. 784 pixels): A_1 = X Omega_1 by the tiled GEMM
+  // (k_step_agemm), in row chunks of <= 64M floats of stream-ordered scratch, read by layer 0
+  // instead of a d-long k-step loop per feature chunk (needs one Omega_1 for all chains)
+  const bool wide0 = pl.d[0] > 32 && (!pl.hyp_per_chain || pl.n_chains == 1) && pl.n_rf[0] % 4 == 0 &&
+                     (int64_t)pl.d[0] * pl.n_rf[0] < ((int64_t)1 << 29) &&
+                     !getenv("DGPRF_FORWARD_NO_AGEMM");
+  // tile kernel: d <= 32 (layer 0 exempt when wide0 and no input concatenation), g <= 64,
+  // R % 4 == 0 in every layer
+  bool tiles = (pl.d_in <= 32) || (wide0 && !pl.input_cat);
   for (int l = 0; l < pl.n_layers; ++l)
-    tiles = tiles && pl.d[l] <= 32 && pl.n_gp[l] <= 64 && pl.n_rf[l] % 4 == 0 &&
-            (int64_t)2 * pl.n_rf[l] * pl.n_gp[l] < ((int64_t)1 << 29);
-  if (tiles && !getenv("DGPRF_FORWARD_ROWS")) {
-    int gmax = 1, dmax = 1;
-    for (int l = 0; l < pl.n_layers; ++l) {
-      gmax = max(gmax, pl.n_gp[l]);
-      dmax = max(dmax, pl.d[l]);
+    tiles = tiles && (pl.d[l] <= 32 || (l == 0 && wide0)) && pl.n_gp[l] <= 64 &&
+            pl.n_rf[l] % 4 == 0 && (int64_t)2 * pl.n_rf[l] * pl.n_gp[l] < ((int64_t)1 << 29);
+  tiles = tiles && !getenv("DGPRF_FORWARD_ROWS");
+  const int64_t R0 = pl.n_rf[0];
+  const int64_t chunk = wide0 ? std::max<int64_t>(32, std::min<int64_t>((((int64_t)1 << 26) / R0) / 32 * 32,
+                                                                     (n + 31) / 32 * 32))
+                              : n;
+  float* a0 = nullptr;
+  if (wide0) {
+    hipError_t e = hipMallocAsync((void**)&a0, (size_t)chunk * R0 * sizeof(float), s);
+    if (e != hipSuccess) return e;
+  }
+  hipError_t err = hipSuccess;
+  for (int64_t r0 = 0; r0 < n && err == hipSuccess; r0 += chunk) {
+    const int64_t r1 = std::min(n, r0 + chunk);
+    if (wide0) {
+      err = launch_agemm(X + r0 * pl.d_in, r1 - r0, pl.d_in, pl.d[0], omega + pl.omega_off[0],
+                         (int)R0, a0, s);
+      if (err != hipSuccess) break;
     }
-    const int njw = gmax <= 8 ? 1 : (gmax <= 16 ? 2 : (gmax <= 32 ? 4 : 8));  // >= 32 g / 256
-    // >= 16 d / 256; the wide-g instances are compiled with JO = 2 only (host and kernel must size
-    // the LDS ring identically)
-    const int njo = (dmax <= 16 && njw <= 2) ? 1 : 2;
-    const int ntm = njw <= 2 ? 1 : (njw == 4 ? 2 : 4);
-    const int tpw = getenv("DGPRF_TILE_TPW") ? atoi(getenv("DGPRF_TILE_TPW")) == 2 ? 2 : 1 : DGPRF_TILE_TPW_DEFAULT;
-    const TileLds T = tile_lds(pl, ntm, njo, tpw);
-    dim3 tgrid((unsigned)((n + TW_ROWS * tpw - 1) / (TW_ROWS * tpw)), pl.n_chains);
-    size_t tl = (size_t)T.total * sizeof(float);
-    if (const char* pad = getenv("DGPRF_TILE_LDS_BYTES")) tl = max(tl, (size_t)atol(pad));  // experiments
+    const int64_t nr = r1 - r0;
+    if (tiles) {
+      int gmax = 1, dmax = 1;
+      for (int l = 0; l < pl.n_layers; ++l) {
+        gmax = max(gmax, pl.n_gp[l]);
+        if (!(l == 0 && wide0)) dmax = max(dmax, pl.d[l]);  // Omega rows staged per block
+      }
+      const int njw = gmax <= 8 ? 1 : (gmax <= 16 ? 2 : (gmax <= 32 ? 4 : 8));  // >= 32 g / 256
+      // >= 16 d / 256; the wide-g instances are compiled with JO = 2 only (host and kernel must
+      // size the LDS ring identically)
+      const int njo = (dmax <= 16 && njw <= 2) ? 1 : 2;
+      const int ntm = njw <= 2 ? 1 : (njw == 4 ? 2 : 4);
+      const int tpw = getenv("DGPRF_TILE_TPW") ? atoi(getenv("DGPRF_TILE_TPW")) == 2 ? 2 : 1 : DGPRF_TILE_TPW_DEFAULT;
+      const TileLds T = tile_lds(pl, ntm, njo, tpw, wide0);
+      dim3 tgrid((unsigned)((nr + TW_ROWS * tpw - 1) / (TW_ROWS * tpw)), pl.n_chains);
+      size_t tl = (size_t)T.total * sizeof(float);
+      if (const char* pad = getenv("DGPRF_TILE_LDS_BYTES")) tl = max(tl, (size_t)atol(pad));  // experiments
+#define DGPRF_TILE_LAUNCH1(NM, J, JO, TP, WD)                                                      \
+  do {                                                                                             \
+    set_lds_limit((const void*)k_forward_tiles<NM, J, JO, TP, WD>, tl);                            \
+    hipLaunchKernelGGL((k_forward_tiles<NM, J, JO, TP, WD>), tgrid, dim3(TW_THREADS), tl, s, pl,   \
+                       theta, omega, der, X, Y, y_cols, n, fo, logp, se, lse_m, lse_s, se_sum, a0, \
+                       r0, r1);                                                                    \
+  } while (0)
 #define DGPRF_TILE_LAUNCH(NM, J, JO)                                                               \
   do {                                                                                             \
-    if (tpw == 2) {                                                                                \
-      set_lds_limit((const void*)k_forward_tiles<NM, J, JO, 2>, tl);                               \
-      hipLaunchKernelGGL((k_forward_tiles<NM, J, JO, 2>), tgrid, dim3(TW_THREADS), tl, s, pl, theta, \
-                         omega, der, X, Y, y_cols, n, fo, logp, se, lse_m, lse_s, se_sum);         \
-    } else {                                                                                       \
-      set_lds_limit((const void*)k_forward_tiles<NM, J, JO, 1>, tl);                               \
-      hipLaunchKernelGGL((k_forward_tiles<NM, J, JO, 1>), tgrid, dim3(TW_THREADS), tl, s, pl, theta, \
-                         omega, der, X, Y, y_cols, n, fo, logp, se, lse_m, lse_s, se_sum);         \
-    }                                                                                              \
+    if (wide0) DGPRF_TILE_LAUNCH1(NM, J, JO, 1, true);                                             \
+    else if (tpw == 2) DGPRF_TILE_LAUNCH1(NM, J, JO, 2, false);                                    \
+    else DGPRF_TILE_LAUNCH1(NM, J, JO, 1, false);                                                  \
   } while (0)
-    if (njw == 1) {
-      if (njo == 1) DGPRF_TILE_LAUNCH(1, 1, 1);
-      else DGPRF_TILE_LAUNCH(1, 1, 2);
-    } else if (njw == 2) {
-      if (njo == 1) DGPRF_TILE_LAUNCH(1, 2, 1);
-      else DGPRF_TILE_LAUNCH(1, 2, 2);
-    } else if (njw == 4) {
-      DGPRF_TILE_LAUNCH(2, 4, 2);
-    } else {
-      DGPRF_TILE_LAUNCH(4, 8, 2);
-    }
+      if (njw == 1) {
+        if (njo == 1) DGPRF_TILE_LAUNCH(1, 1, 1);
+        else DGPRF_TILE_LAUNCH(1, 1, 2);
+      } else if (njw == 2) {
+        if (njo == 1) DGPRF_TILE_LAUNCH(1, 2, 1);
+        else DGPRF_TILE_LAUNCH(1, 2, 2);
+      } else if (njw == 4) {
+        DGPRF_TILE_LAUNCH(2, 4, 2);
+      } else {
+        DGPRF_TILE_LAUNCH(4, 8, 2);
+      }
 #undef DGPRF_TILE_LAUNCH
-    return hipGetLastError();
-  }
-  dim3 grid((unsigned)((n + TR - 1) / TR), pl.n_chains);
-  const size_t lds = (size_t)LD.total * sizeof(float);
+#undef DGPRF_TILE_LAUNCH1
+    } else {
+      const size_t lds = (size_t)LD.total * sizeof(float);
+      dim3 grid((unsigned)((nr + TR - 1) / TR), pl.n_chains);
 #define DGPRF_FWD_LAUNCH(S, NM)                                                                    \
   do {                                                                                             \
     set_lds_limit((const void*)k_forward_rows<S, NM>, lds);                                        \
     hipLaunchKernelGGL((k_forward_rows<S, NM>), grid, dim3(256), lds, s, pl, theta, omega, der, X, \
-                       Y, y_cols, n, fo, logp, se, lse_m, lse_s, se_sum);                          \
+                       Y, y_cols, n, fo, logp, se, lse_m, lse_s, se_sum, a0, r0, r1);             \
   } while (0)
-  if (smalld) {
-    if (notmax == 1) DGPRF_FWD_LAUNCH(true, 1);
-    else if (notmax == 2) DGPRF_FWD_LAUNCH(true, 2);
-    else DGPRF_FWD_LAUNCH(true, 4);
-  } else {
-    if (notmax == 1) DGPRF_FWD_LAUNCH(false, 1);
-    else if (notmax == 2) DGPRF_FWD_LAUNCH(false, 2);
-    else DGPRF_FWD_LAUNCH(false, 4);
-  }
+      if (smalld) {
+        if (notmax == 1) DGPRF_FWD_LAUNCH(true, 1);
+        else if (notmax == 2) DGPRF_FWD_LAUNCH(true, 2);
+        else DGPRF_FWD_LAUNCH(true, 4);
+      } else {
+        if (notmax == 1) DGPRF_FWD_LAUNCH(false, 1);
+        else if (notmax == 2) DGPRF_FWD_LAUNCH(false, 2);
+        else DGPRF_FWD_LAUNCH(false, 4);
+      }
 #undef DGPRF_FWD_LAUNCH
-  return hipGetLastError();
+    }
+    err = hipGetLastError();
+  }
+  if (a0) {
+    const hipError_t e = hipFreeAsync(a0, s);
+    if (err == hipSuccess) err = e;
+  }
+  return err;
 }
 
 size_t forward_rows_lds_bytes(const dgprf_plan_t& pl) {

@@ -1744,6 +1744,25 @@ hipError_t launch_step_update(const dgprf_plan_t& pl, const StepDev& sd, const U
 }
 
 
+hipError_t launch_agemm(const float* X, int64_t n, int ld, int d, const float* om, int R,
+                        float* aout, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if (n > INT32_MAX || (int64_t)n * ld >= ((int64_t)1 << 29) || (int64_t)d * R >= ((int64_t)1 << 29))
+    return hipErrorInvalidValue;  // 32-bit buffer offsets
+  AgemmK g;
+  g.xrows = X;
+  g.om = om;
+  g.aout = aout;
+  g.xrow_cs = g.om_cs = g.ws_cs = 0;
+  g.B = (int32_t)n;
+  g.d = d;
+  g.R = R;
+  g.d_in = ld;
+  dim3 grid((unsigned)((R + 63) / 64), (unsigned)((n + 31) / 32), 1);
+  hipLaunchKernelGGL(k_step_agemm, grid, dim3(256), 0, s, g);
+  return hipGetLastError();
+}
+
 hipError_t launch_gather(const dgprf_plan_t& pl, const StepDev& sd, hipStream_t s) {
   if (sd.bd.mode == DGPRF_BATCH_DIRECT) return hipSuccess;
   GatherK a;
