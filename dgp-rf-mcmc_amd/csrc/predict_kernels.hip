@@ -941,8 +941,10 @@ hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const
             pl.n_rf[l] % 4 == 0 && (int64_t)2 * pl.n_rf[l] * pl.n_gp[l] < ((int64_t)1 << 29);
   tiles = tiles && !getenv("DGPRF_FORWARD_ROWS");
   const int64_t R0 = pl.n_rf[0];
-  const int64_t chunk = wide0 ? std::max<int64_t>(32, std::min<int64_t>((((int64_t)1 << 26) / R0) / 32 * 32,
-                                                                     (n + 31) / 32 * 32))
+  int64_t chunk_cap = (((int64_t)1 << 26) / R0) / 32 * 32;
+  if (const char* c = getenv("DGPRF_AGEMM_CHUNK_ROWS"))  // tests: force several chunks
+    chunk_cap = std::max<int64_t>(32, atol(c) / 32 * 32);
+  const int64_t chunk = wide0 ? std::max<int64_t>(32, std::min<int64_t>(chunk_cap, (n + 31) / 32 * 32))
                               : n;
   float* a0 = nullptr;
   if (wide0) {

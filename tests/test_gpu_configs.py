@@ -140,3 +140,71 @@ def test_config_graph_steps_finite_and_deterministic(dev, cfg):
         out.append(m._engine.theta.clone())
         assert torch.isfinite(out[-1]).all()
     assert torch.equal(out[0], out[1])
+
+
+@pytest.mark.parametrize("chunk_rows", [None, "64"])
+def test_wide_first_layer_forward_chunks(dev, monkeypatch, chunk_rows):
+    """Wide first layer (d = 40 > 32): the A_1 GEMM + tile kernel, in one chunk and in 64-row chunks
+    (DGPRF_AGEMM_CHUNK_ROWS) over a ragged 201-row set, and through the row kernel; per-layer F and
+    the LSE accumulators against the oracle."""
+    from dgprf import engine as E
+    from dgprf.predictive import PredictiveLSE
+    from likelihoods import Gaussian
+    from models.dgp import DGP_RF
+    if chunk_rows:
+        monkeypatch.setenv("DGPRF_AGEMM_CHUNK_ROWS", chunk_rows)
+    E.set_seed(51)
+    kinds, n_rf, n_gp = ["RBF", "ARC", "RBF"], [96, 64, 48], [12, 6, 2]
+    m = DGP_RF(40, 2, n_hidden_layers=3, n_rf=n_rf, n_gp=n_gp, likelihood=Gaussian(variance=0.2),
+               kernel_type_list=kinds)
+    p = O.Params(40, 2, n_rf, n_gp, kinds, "gaussian", False,
+                 z=[cpu(m.BNN.layers[2 * l].z) for l in range(3)], W=[cpu(w) for w in m.W_mcmc],
+                 log_inv_ls=[cpu(k.log_inv_length_scale) for k in m.kernel_list],
+                 lik_log_var=np.log(0.2))
+    rng = np.random.default_rng(8)
+    X = rng.standard_normal((201, 40)).astype(np.float32).astype(np.float64)
+    Y = rng.standard_normal((201, 2)).astype(np.float32).astype(np.float64)
+    for rows in (False, True):
+        if rows:
+            monkeypatch.setenv("DGPRF_FORWARD_ROWS", "1")
+        outs = m._engine.forward(X, f_out="all")["F"]
+        _, cache = O.forward(p, X, keep=True)
+        for l in range(3):
+            assert rel_err(cpu(outs[l][0]), cache[l][2] @ p.W[l]) < 5e-5, (rows, l)
+        acc = PredictiveLSE(m._engine, X, Y)
+        acc.add_sample()
+        ll, rmse = acc.finalize()
+        lp, se = O.eval_log_likelihood_and_se(p, X, Y)
+        ref_ll, ref_rmse = O.predictive_summary(lp[None], se[None])
+        assert abs(ll - ref_ll) < 1e-4 and abs(rmse - ref_rmse) < 1e-5 * max(1.0, ref_rmse)
+    monkeypatch.delenv("DGPRF_FORWARD_ROWS")
+
+
+def test_wide_first_layer_full_bayes_grad(dev):
+    """full_bayesian=True gradients of a model whose first layer is wide (d = 40): the backward reads
+    the precomputed A_1 and the X tile for the hyper-parameter sums."""
+    from dgprf import engine as E
+    from likelihoods import Softmax
+    from models.dgp import DGP_RF
+    from test_gpu_full_bayes import group_err
+    E.set_seed(52)
+    kinds, n_rf, n_gp = ["RBF", "RBF"], [64, 48], [6, 4]
+    m = DGP_RF(40, 4, n_hidden_layers=2, n_rf=n_rf, n_gp=n_gp, likelihood=Softmax(),
+               kernel_type_list=kinds)
+    p = O.Params(40, 4, n_rf, n_gp, kinds, "softmax", False,
+                 z=[cpu(m.BNN.layers[2 * l].z) for l in range(2)], W=[cpu(w) for w in m.W_mcmc],
+                 log_inv_ls=[cpu(k.log_inv_length_scale) for k in m.kernel_list])
+    rng = np.random.default_rng(9)
+    X = rng.uniform(-1, 1, (37, 40)).astype(np.float32).astype(np.float64)
+    Y = rng.integers(0, 4, (37, 1)).astype(float)
+    eng = m._engine
+    G = eng.grad(X, Y, 5000, full_bayes=True)
+    ref = O.grad_full(p, X, Y, 5000, O.Trainable(kernel=True, lik=False, mean=False))
+    Gw = unpack(eng, G[:, :eng.layout.w_total])
+    pl = eng.layout
+    h = cpu(G[0, pl.w_total:])
+    for l in range(2):
+        assert rel_err(Gw[l], ref["W"][l]) < 2e-4, ("W", l)
+        lis = h[pl.lis_off[l]:pl.lis_off[l] + pl.d[l]]
+        assert group_err(lis, ref["log_inv_ls"][l]) < 5e-4, ("lis", l)
+    assert group_err([h[0], h[1]], [ref["log_amp"][0], ref["log_amp"][1]]) < 5e-4
