@@ -124,6 +124,72 @@ def test_config_predictive_rows(dev, cfg):
     assert np.max(np.abs(lp - ref)) < 2e-5 * max(1.0, np.max(np.abs(ref)))
 
 
+def test_predictive_multi_round_rows(dev):
+    """Config 2's shape (3-layer RBF, n_rf 1024, g [8,8,1]) over 70,001 test rows: more tiles than
+    one round of resident waves (65,536 rows on 256 CUs) plus a ragged remainder; per-row log p
+    against the oracle, and bit-identical on a second launch."""
+    c = dict(kinds=["RBF"] * 3, n_rf=[1024] * 3, n_gp=[8, 8, 1], D=8, lik="gaussian")
+    m, p = _model(c, 61)
+    Xt, Yt = _data(c, 70_001, 62)
+    lp = cpu(m._engine.forward(Xt, Yt, logp=True)["logp"][0])
+    ref = O.log_prob(p, O.forward(p, Xt), Yt)
+    assert np.max(np.abs(lp - ref)) < 2e-5 * max(1.0, np.max(np.abs(ref)))
+    assert np.array_equal(lp, cpu(m._engine.forward(Xt, Yt, logp=True)["logp"][0]))
+
+
+@pytest.mark.parametrize("cfg", [3, 5])
+def test_config_sghmc_step_injected_noise(dev, cfg):
+    c = CONFIGS[cfg]
+    m, p = _model(c, 20 + cfg)
+    eng = m._engine
+    X, Y = _data(c, 2 * c["B"], 100 + cfg)
+    X, Y = _rows_off_kinks(c, p, X, Y, c["B"])
+    L = len(c["kinds"])
+    rng = np.random.default_rng(cfg)
+    m.precond_update(None, 1000, precond_type="identity")
+    m0 = [cpu(eng.mom_view(l)).astype(np.float64) for l in range(L)]
+    xi = [rng.standard_normal(w.shape) for w in p.W]
+    eng.step(X, Y, 1000, 0.01, 0.9, 1.0, xi=pack(eng, xi))
+    O.sgmcmc_step(p, m0, X, Y, 1000, 0.01, 0.9, 1.0, [1.0] * L, xi)
+    for l in range(L):
+        assert rel_err(cpu(eng.W_view(l)), p.W[l]) < 2e-5, (cfg, l)
+
+
+@pytest.mark.parametrize("cfg", [3, 4, 5])
+def test_config_predictive_rows(dev, cfg):
+    """eval_log_likelihood(_and_se) over a test set (tile kernel for configs 3 and 5, the general
+    row kernel for config 4's D = 784) against the oracle, row by row."""
+    c = CONFIGS[cfg]
+    m, p = _model(c, 30 + cfg)
+    Xt, Yt = _data(c, c["n_test"], 200 + cfg)
+    out = m._engine.forward(Xt, Yt, logp=True)
+    lp = cpu(out["logp"][0])
+    ref = O.log_prob(p, O.forward(p, Xt), Yt)
+    assert np.max(np.abs(lp - ref)) < 2e-5 * max(1.0, np.max(np.abs(ref)))
+
+
+@pytest.mark.parametrize("no_pair", [None, "1"])
+def test_predictive_tail_split_rows(dev, monkeypatch, no_pair):
+    """Config 2's shape (3-layer RBF, n_rf 1024, g [8,8,1]) over 70,001 test rows: one full round of
+    one-tile-per-wave tiles (65,536 rows on 256 CUs) plus a ragged remainder that runs as wave pairs
+    (default) or as single waves (DGPRF_TILE_NO_PAIR); per-row log p against the oracle, and the two
+    launch shapes bit-identical row by row."""
+    c = dict(kinds=["RBF"] * 3, n_rf=[1024] * 3, n_gp=[8, 8, 1], D=8, lik="gaussian")
+    m, p = _model(c, 61)
+    Xt, Yt = _data(c, 70_001, 62)
+    if no_pair:
+        monkeypatch.setenv("DGPRF_TILE_NO_PAIR", no_pair)
+    lp = cpu(m._engine.forward(Xt, Yt, logp=True)["logp"][0])
+    ref = O.log_prob(p, O.forward(p, Xt), Yt)
+    assert np.max(np.abs(lp - ref)) < 2e-5 * max(1.0, np.max(np.abs(ref)))
+    monkeypatch.setenv("DGPRF_TILE_NO_PAIR", "1")
+    lp1 = cpu(m._engine.forward(Xt, Yt, logp=True)["logp"][0])
+    monkeypatch.delenv("DGPRF_TILE_NO_PAIR")
+    lp2 = cpu(m._engine.forward(Xt, Yt, logp=True)["logp"][0])
+    assert np.array_equal(lp, lp1 if no_pair else lp2)
+    assert np.max(np.abs(lp1 - lp2)) < 2e-5 * max(1.0, np.max(np.abs(ref)))
+
+
 @pytest.mark.parametrize("cfg", [3, 5])
 def test_config_graph_steps_finite_and_deterministic(dev, cfg):
     """200 graph-replayed steps with on-device minibatches at the config's N (config 5 scaled to
