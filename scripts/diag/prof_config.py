@@ -1,4 +1,5 @@
-"""Diagnostic: per-kernel event times of one SGHMC step for a BASELINE config (default 4)."""
+"""Diagnostic: per-kernel event times of one SGHMC step for a BASELINE config (default 4), and the
+predictive us/sample over the config's test-set size (capped at 100k rows)."""
 import os
 import sys
 
@@ -30,3 +31,21 @@ print(f"config {cfg}: empty pair {e * 1e3:.2f} us")
 print("fwd  us:", [round((x - e) * 1e3, 2) for x in prof["fwd"]])
 print("bwd  us:", [round((x - e) * 1e3, 2) for x in prof["bwd"]])
 print("upd  us:", round((prof["update"] - e) * 1e3, 2))
+
+from dgprf.predictive import PredictiveLSE  # noqa: E402
+nt = min(c["n_test"], 100_000)
+if c["likelihood"] == "softmax":
+    Xt, Yt = classification_data(nt, c["d_in"], c["d_out"], seed=1, device=dev)
+else:
+    Xt, Yt, _ = regression_data(nt, c["d_in"], seed=1, device=dev)
+acc = PredictiveLSE(m._engine, Xt, Yt)
+acc.add_sample()
+acc.add_sample()
+torch.cuda.synchronize()
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record()
+for _ in range(10):
+    acc.add_sample(build=False)
+e1.record()
+torch.cuda.synchronize()
+print(f"predictive us/sample (n_test={nt}): {e0.elapsed_time(e1) / 10 * 1e3:.1f}")
