@@ -49,6 +49,18 @@ def pred_flops(n, d, R, P, g):
     return n * sum(2 * (d[l] * R[l] + P[l] * g[l]) for l in range(len(d)))
 
 
+def cpu_model():
+    """`model name` of the host CPU (/proc/cpuinfo, as lscpu reports it)."""
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def cpu_baseline(seconds):
     """The reference algorithm, op for op, on the host (oracle/dgp_oracle.py in float32 numpy):
     TensorFlow is not installed here or on the GPU box, so this restatement is the CPU proxy."""
@@ -83,6 +95,7 @@ def cpu_baseline(seconds):
     pred_rate = reps / (time.perf_counter() - t0) / (CFG["N_test"] / 10_000)
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     return {"value": round(step_rate, 2), "unit": "steps/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
             "sample": f"{steps} SGHMC steps of config 2 (B=200, L=3, n_rf=1024, float32 numpy "
                       f"op-for-op restatement of models/dgp.py:184-216, injected N(0,1) noise); "
                       f"predictive on a 10k-row slice scaled to 1e5 rows",
@@ -223,7 +236,14 @@ def main():
                steps_per_graph=args.steps_per_graph, perm_seed=rank_seed(0, rank))
 
     # ---------------- SGHMC steps (graph-replayed, on-device minibatching)
-    model.run_sgmcmc(X, Y, N_, args.warmup, **run)
+    # Every hipGraph the timed call replays is captured, instantiated and launched once here
+    # (untimed), so the timed region is replays only; then the W warm-up steps.
+    timed_plan = model.sgmcmc_graphs(X, Y, N_, args.steps, **run)
+    timed_graphs = [{"steps_per_graph": gph.steps, "replays": reps} for gph, reps in timed_plan]
+    for gph, _ in timed_plan:
+        gph.launch()
+    if args.warmup > 0:
+        model.run_sgmcmc(X, Y, N_, args.warmup, **run)
     barrier_sync()
     es0, es1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
@@ -366,7 +386,10 @@ def main():
             "config": {"workload": "config2: 3-layer RBF-RF DGP, n_rf=1024 (Phi 2048), g=[8,8,1], "
                                    "D=8, N=1e6, B=200, Gaussian s2=0.1, SGHMC lr=0.01 beta=0.9 T=1, "
                                    "W-only, identity preconditioner",
-                       "chains_per_gpu": 1, "steps_per_graph": args.steps_per_graph,
+                       "chains_per_gpu": 1,
+                       "timed_graphs": timed_graphs,
+                       "timed_region": "hipGraph replays only: every graph it replays was "
+                                       "captured and launched once before the clock",
                        "parallelism": f"chain-parallel x{world} (independent chains, RCCL "
                                       "all-gather of predictive accumulators only)"},
             "predictive_samples_per_s": round(pred_per_s, 3),

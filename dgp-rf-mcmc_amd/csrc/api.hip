@@ -155,6 +155,8 @@ int dgprf_plan_init(dgprf_plan_t* pl) {
   if (L < 1 || L > DGPRF_MAX_LAYERS) return DGPRF_E_SHAPE;
   if (pl->d_in < 1 || pl->d_out < 1 || pl->batch < 1 || pl->n_chains < 1) return DGPRF_E_SHAPE;
   if (pl->likelihood != DGPRF_LIK_GAUSSIAN && pl->likelihood != DGPRF_LIK_SOFTMAX) return DGPRF_E_ARG;
+  if (pl->fwd_path < DGPRF_FWD_AUTO || pl->fwd_path > DGPRF_FWD_NO_AGEMM || pl->agemm_chunk_rows < 0)
+    return DGPRF_E_ARG;
   for (int l = 0; l < L; ++l) {
     if (pl->kind[l] != DGPRF_RBF && pl->kind[l] != DGPRF_ARC) return DGPRF_E_ARG;
     if (pl->n_rf[l] < 1 || pl->n_gp[l] < 1 || pl->n_gp[l] > DGPRF_MAX_G) return DGPRF_E_SHAPE;
@@ -411,10 +413,18 @@ int dgprf_profile_step(const dgprf_plan_t* plan, const dgprf_chain_t* chain,
   return hip_rc(e);
 }
 
+int dgprf_forward_scratch(const dgprf_plan_t* plan, int64_t n, int64_t* floats_out) {
+  int rc = check_plan(plan);
+  if (rc) return rc;
+  if (!floats_out || n < 0) return DGPRF_E_ARG;
+  *floats_out = dgprf::forward_cfg(*plan, n).scratch_floats;
+  return DGPRF_OK;
+}
+
 int dgprf_forward(const dgprf_plan_t* plan, const float* theta, const float* omega,
                   const float* der, const float* X, const float* Y, int32_t y_cols, int64_t n,
                   float* const* f_out, float* logp, float* se, float* lse_m, float* lse_s,
-                  float* se_sum, void* stream) {
+                  float* se_sum, float* scratch, int64_t scratch_floats, void* stream) {
   int rc = check_plan(plan);
   if (rc) return rc;
   if (!theta || !omega || !der || n < 0 || (n > 0 && !X)) return DGPRF_E_ARG;
@@ -424,8 +434,10 @@ int dgprf_forward(const dgprf_plan_t* plan, const float* theta, const float* ome
   if (se && plan->likelihood != DGPRF_LIK_GAUSSIAN) return DGPRF_E_ARG;
   if (lik && plan->likelihood == DGPRF_LIK_GAUSSIAN && y_cols < plan->n_gp[plan->n_layers - 1])
     return DGPRF_E_SHAPE;
+  if (scratch_floats < 0 || (scratch_floats > 0 && !scratch)) return DGPRF_E_ARG;
+  if (scratch_floats < dgprf::forward_cfg(*plan, n).scratch_floats) return DGPRF_E_ARG;
   return hip_rc(dgprf::launch_forward_rows(*plan, theta, omega, der, X, Y, y_cols, n, f_out, logp,
-                                           se, lse_m, lse_s, se_sum, as_stream(stream)));
+                                           se, lse_m, lse_s, se_sum, scratch, as_stream(stream)));
 }
 
 int dgprf_lse_finalize(const float* lse_m, const float* lse_s, const float* se_sum, int32_t parts,

@@ -98,10 +98,19 @@ hipError_t launch_agemm(const float* X, int64_t n, int ld, int d, const float* o
                         float* aout, hipStream_t s);
 hipError_t launch_advance(int64_t* step, int64_t by, hipStream_t s);
 
+// How dgprf_forward covers n rows: tile or row kernel, the A_1 GEMM for a wide first layer (in
+// row chunks of `chunk` rows of caller scratch).  Host-only, shared by the launcher and the
+// scratch query so both size the chunks identically.
+struct ForwardCfg {
+  bool wide0, tiles;
+  int64_t chunk, scratch_floats;
+};
+ForwardCfg forward_cfg(const dgprf_plan_t& pl, int64_t n);
 hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const float* omega,
                                const float* der, const float* X, const float* Y, int y_cols,
                                int64_t n, float* const* f_out, float* logp, float* se,
-                               float* lse_m, float* lse_s, float* se_sum, hipStream_t s);
+                               float* lse_m, float* lse_s, float* se_sum, float* scratch,
+                               hipStream_t s);
 hipError_t launch_lse_finalize(const float* lse_m, const float* lse_s, const float* se_sum,
                                int parts, int64_t n, double s_total, float log_y_std, float y_std,
                                float* lse_out, double* out, hipStream_t s);

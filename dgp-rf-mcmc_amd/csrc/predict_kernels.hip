@@ -270,8 +270,10 @@ __global__ __launch_bounds__(256) void k_forward_rows(
         for (int o = 0; o < g; ++o) mx = fmaxf(mx, f[o]);
         float s = 0.f;
         for (int o = 0; o < g; ++o) s += expf(f[o] - mx);
-        const int label = min(max((int)y[0], 0), g - 1);
-        lp = f[label] - (mx + logf(s));
+        // int32(Y[:, 0]) (likelihoods/softmax.py:14); a label outside [0, g) scores NaN (TF raises)
+        const int lab = (int)y[0];
+        const bool lab_ok = lab >= 0 && lab < g;
+        lp = lab_ok ? f[lab] - (mx + logf(s)) : __builtin_nanf("");
       }
       const int64_t idx = (int64_t)chain * n + b;
       if (logp_out) logp_out[idx] = lp;
@@ -637,14 +639,9 @@ __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           if (REV) {
-#ifdef DGPRF_EXP_NOTRIG
-            p0[t][r] = at[t][r];
-            p1[t][r] = at[t][r] * 0.5f;
-#else
             const float u = __builtin_amdgcn_fractf(at[t][r]);
             p0[t][r] = __builtin_amdgcn_cosf(u);
             p1[t][r] = __builtin_amdgcn_sinf(u);
-#endif
           } else if (RBF) {
             float sv, cv;
             rf_sincos(at[t][r], &sv, &cv);
@@ -705,13 +702,8 @@ __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
             const float w1 = RBF ? wl[64 * WST + off] : 0.f;
 #pragma unroll
             for (int t = 0; t < TPW; ++t) {
-#ifdef DGPRF_EXP_NOFMFMA
-              acc[t][ot][r] = fmaf(w0, p0[t][r], acc[t][ot][r]);
-              if (RBF) acs[t][ot][r] = fmaf(w1, p1[t][r], acs[t][ot][r]);
-#else
               acc[t][ot] = mfma16(w0, p0[t][r], acc[t][ot]);
               if (RBF) acs[t][ot] = mfma16(w1, p1[t][r], acs[t][ot]);
-#endif
             }
           }
       }
@@ -884,8 +876,10 @@ void k_forward_tiles(
         for (int o = 0; o < g; ++o) mx = fmaxf(mx, f[o]);
         float s = 0.f;
         for (int o = 0; o < g; ++o) s += expf(f[o] - mx);
-        const int label = min(max((int)y[0], 0), g - 1);
-        lp = f[label] - (mx + logf(s));
+        // int32(Y[:, 0]) (likelihoods/softmax.py:14); a label outside [0, g) scores NaN (TF raises)
+        const int lab = (int)y[0];
+        const bool lab_ok = lab >= 0 && lab < g;
+        lp = lab_ok ? f[lab] - (mx + logf(s)) : __builtin_nanf("");
       }
       const int64_t idx = (int64_t)chain * n + b;
       if (logp_out) logp_out[idx] = lp;
@@ -913,10 +907,33 @@ extern "C" int dgprf_debug_read_pred_stamps(unsigned long long* host, long long 
 
 namespace dgprf {
 
+ForwardCfg forward_cfg(const dgprf_plan_t& pl, int64_t n) {
+  ForwardCfg c;
+  // wide first layer (d_1 > 32, e.g. 784 pixels): A_1 = X Omega_1 by the tiled GEMM
+  // (k_step_agemm), in row chunks of caller-owned scratch, read by layer 0 instead of a d-long
+  // k-step loop per feature chunk (needs one Omega_1 for all chains)
+  c.wide0 = pl.fwd_path != DGPRF_FWD_NO_AGEMM && pl.d[0] > 32 &&
+            (!pl.hyp_per_chain || pl.n_chains == 1) && pl.n_rf[0] % 4 == 0 &&
+            (int64_t)pl.d[0] * pl.n_rf[0] < ((int64_t)1 << 29);
+  // tile kernel: d <= 32 (layer 0 exempt when wide0 and no input concatenation), g <= 64,
+  // R % 4 == 0 in every layer
+  c.tiles = pl.fwd_path != DGPRF_FWD_ROWS && ((pl.d_in <= 32) || (c.wide0 && !pl.input_cat));
+  for (int l = 0; l < pl.n_layers; ++l)
+    c.tiles = c.tiles && (pl.d[l] <= 32 || (l == 0 && c.wide0)) && pl.n_gp[l] <= 64 &&
+              pl.n_rf[l] % 4 == 0 && (int64_t)2 * pl.n_rf[l] * pl.n_gp[l] < ((int64_t)1 << 29);
+  const int64_t R0 = pl.n_rf[0];
+  int64_t cap = (((int64_t)1 << 26) / R0) / 32 * 32;
+  if (pl.agemm_chunk_rows > 0) cap = std::max<int64_t>(32, pl.agemm_chunk_rows / 32 * 32);
+  c.chunk = c.wide0 ? std::max<int64_t>(32, std::min<int64_t>(cap, (n + 31) / 32 * 32)) : n;
+  c.scratch_floats = c.wide0 && n > 0 ? c.chunk * R0 : 0;
+  return c;
+}
+
 hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const float* omega,
                                const float* der, const float* X, const float* Y, int y_cols,
                                int64_t n, float* const* f_out, float* logp, float* se,
-                               float* lse_m, float* lse_s, float* se_sum, hipStream_t s) {
+                               float* lse_m, float* lse_s, float* se_sum, float* scratch,
+                               hipStream_t s) {
   if (n <= 0) return hipSuccess;
   const FwdLds LD = fwd_lds(pl);
   FOut fo;
@@ -927,30 +944,11 @@ hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const
     smalld = smalld && pl.d[l] <= 32;
     notmax = max(notmax, (pl.n_gp[l] + 15) >> 4);
   }
-  // wide first layer (d_1 > 32, e.g. 784 pixels): A_1 = X Omega_1 by the tiled GEMM
-  // (k_step_agemm), in row chunks of <= 64M floats of stream-ordered scratch, read by layer 0
-  // instead of a d-long k-step loop per feature chunk (needs one Omega_1 for all chains)
-  const bool wide0 = pl.d[0] > 32 && (!pl.hyp_per_chain || pl.n_chains == 1) && pl.n_rf[0] % 4 == 0 &&
-                     (int64_t)pl.d[0] * pl.n_rf[0] < ((int64_t)1 << 29) &&
-                     !getenv("DGPRF_FORWARD_NO_AGEMM");
-  // tile kernel: d <= 32 (layer 0 exempt when wide0 and no input concatenation), g <= 64,
-  // R % 4 == 0 in every layer
-  bool tiles = (pl.d_in <= 32) || (wide0 && !pl.input_cat);
-  for (int l = 0; l < pl.n_layers; ++l)
-    tiles = tiles && (pl.d[l] <= 32 || (l == 0 && wide0)) && pl.n_gp[l] <= 64 &&
-            pl.n_rf[l] % 4 == 0 && (int64_t)2 * pl.n_rf[l] * pl.n_gp[l] < ((int64_t)1 << 29);
-  tiles = tiles && !getenv("DGPRF_FORWARD_ROWS");
-  const int64_t R0 = pl.n_rf[0];
-  int64_t chunk_cap = (((int64_t)1 << 26) / R0) / 32 * 32;
-  if (const char* c = getenv("DGPRF_AGEMM_CHUNK_ROWS"))  // tests: force several chunks
-    chunk_cap = std::max<int64_t>(32, atol(c) / 32 * 32);
-  const int64_t chunk = wide0 ? std::max<int64_t>(32, std::min<int64_t>(chunk_cap, (n + 31) / 32 * 32))
-                              : n;
-  float* a0 = nullptr;
-  if (wide0) {
-    hipError_t e = hipMallocAsync((void**)&a0, (size_t)chunk * R0 * sizeof(float), s);
-    if (e != hipSuccess) return e;
-  }
+  const ForwardCfg cfg = forward_cfg(pl, n);
+  const bool wide0 = cfg.wide0, tiles = cfg.tiles;
+  const int64_t chunk = cfg.chunk, R0 = pl.n_rf[0];
+  float* a0 = wide0 ? scratch : nullptr;
+  if (wide0 && !a0) return hipErrorInvalidValue;
   hipError_t err = hipSuccess;
   for (int64_t r0 = 0; r0 < n && err == hipSuccess; r0 += chunk) {
     const int64_t r1 = std::min(n, r0 + chunk);
@@ -971,11 +969,10 @@ hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const
       // size the LDS ring identically)
       const int njo = (dmax <= 16 && njw <= 2) ? 1 : 2;
       const int ntm = njw <= 2 ? 1 : (njw == 4 ? 2 : 4);
-      const int tpw = getenv("DGPRF_TILE_TPW") ? atoi(getenv("DGPRF_TILE_TPW")) == 2 ? 2 : 1 : DGPRF_TILE_TPW_DEFAULT;
+      constexpr int tpw = DGPRF_TILE_TPW_DEFAULT;
       const TileLds T = tile_lds(pl, ntm, njo, tpw, wide0);
       dim3 tgrid((unsigned)((nr + TW_ROWS * tpw - 1) / (TW_ROWS * tpw)), pl.n_chains);
-      size_t tl = (size_t)T.total * sizeof(float);
-      if (const char* pad = getenv("DGPRF_TILE_LDS_BYTES")) tl = max(tl, (size_t)atol(pad));  // experiments
+      const size_t tl = (size_t)T.total * sizeof(float);
 #define DGPRF_TILE_LAUNCH1(NM, J, JO, TP, WD)                                                      \
   do {                                                                                             \
     set_lds_limit((const void*)k_forward_tiles<NM, J, JO, TP, WD>, tl);                            \
@@ -986,8 +983,7 @@ hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const
 #define DGPRF_TILE_LAUNCH(NM, J, JO)                                                               \
   do {                                                                                             \
     if (wide0) DGPRF_TILE_LAUNCH1(NM, J, JO, 1, true);                                             \
-    else if (tpw == 2) DGPRF_TILE_LAUNCH1(NM, J, JO, 2, false);                                    \
-    else DGPRF_TILE_LAUNCH1(NM, J, JO, 1, false);                                                  \
+    else DGPRF_TILE_LAUNCH1(NM, J, JO, tpw, false);                                                \
   } while (0)
       if (njw == 1) {
         if (njo == 1) DGPRF_TILE_LAUNCH(1, 1, 1);
@@ -1023,10 +1019,6 @@ hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const
 #undef DGPRF_FWD_LAUNCH
     }
     err = hipGetLastError();
-  }
-  if (a0) {
-    const hipError_t e = hipFreeAsync(a0, s);
-    if (err == hipSuccess) err = e;
   }
   return err;
 }

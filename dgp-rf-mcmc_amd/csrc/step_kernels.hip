@@ -608,12 +608,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NOT == 1 &
           float se = 0.f;
           for (int o = 0; o < g; ++o) se += expf(df[o] - mx);
           const float lse = mx + logf(se);
-          const int label = min(max((int)y[0], 0), g - 1);
+          // int32(Y[:, 0]) (likelihoods/softmax.py:14); a label outside [0, g) poisons log p and
+          // the gradient with NaN instead of scoring a clamped class (TF raises on it)
+          const int label = (int)y[0];
+          const float bad = (label >= 0 && label < g) ? 0.f : __builtin_nanf("");
           for (int o = 0; o < g; ++o) {
             const float f = df[o];
             if (o == label) logp = f - lse;
-            df[o] = (expf(f - lse) - (o == label ? 1.f : 0.f)) * invB;
+            df[o] = (expf(f - lse) - (o == label ? 1.f : 0.f)) * invB + bad;
           }
+          logp += bad;
         }
         if (sl == 0) a.logp[(int64_t)chain * a.ws_cs + b] = logp;
       }

@@ -22,7 +22,8 @@ RNG_NOISE, RNG_RESAMPLE, RNG_Z, RNG_W, RNG_MOMENTS = 1, 2, 3, 4, 5
 RNG_HYPER, RNG_HYPER_RESAMPLE = 6, 7
 HYP_KERNEL, HYP_LIK, HYP_MEAN = 1, 2, 4
 HMASS = 32  # hmass slots: log_amp l -> l, log_inv_ls l -> 8 + l, mean l -> 16 + l, lik_log_var -> 24
-ABI_VERSION = 3
+ABI_VERSION = 4
+FWD_AUTO, FWD_ROWS, FWD_NO_AGEMM = 0, 1, 2
 
 E_ARG, E_SHAPE, E_HIP, E_PLAN = -1, -2, -3, -4
 
@@ -41,6 +42,7 @@ class Plan(ctypes.Structure):
         ("likelihood", _i32), ("batch", _i32), ("n_chains", _i32),
         ("kind", _i32 * _L), ("n_rf", _i32 * _L), ("n_gp", _i32 * _L),
         ("hyp_flags", _i32), ("hyp_per_chain", _i32), ("ard", _i32 * _L),
+        ("fwd_path", _i32), ("agemm_chunk_rows", _i32),
         ("initialised", _i32),
         ("d", _i32 * _L), ("P", _i32 * _L), ("ns", _i32 * _L), ("cpw", _i32 * _L),
         ("n_row_tiles", _i32), ("n_rt_pad", _i32),
@@ -95,8 +97,9 @@ SIGNATURES = {
     "dgprf_graph_destroy": (_i32, [_vp]),
     "dgprf_profile_step": (_i32, [ctypes.POINTER(Plan), ctypes.POINTER(Chain),
                                   ctypes.POINTER(Batch), ctypes.POINTER(Step), _i32, _vp, _vp]),
+    "dgprf_forward_scratch": (_i32, [ctypes.POINTER(Plan), _i64, ctypes.POINTER(_i64)]),
     "dgprf_forward": (_i32, [ctypes.POINTER(Plan), _vp, _vp, _vp, _vp, _vp, _i32, _i64,
-                             ctypes.POINTER(_vp), _vp, _vp, _vp, _vp, _vp, _vp]),
+                             ctypes.POINTER(_vp), _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp]),
     "dgprf_lse_finalize": (_i32, [_vp, _vp, _vp, _i32, _i64, ctypes.c_double, ctypes.c_float,
                                   ctypes.c_float, _vp, _vp, _vp]),
     "dgprf_rf_omega": (_i32, [_i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),

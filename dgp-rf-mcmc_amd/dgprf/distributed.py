@@ -31,12 +31,16 @@ def gather_accumulators(m, s, e, S_local, group=None):
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
         return m, s, e, S_local
     W = dist.get_world_size(group)
+    # RCCL ("nccl") gathers device tensors over xGMI; gloo (CPU tests, or several ranks sharing one
+    # GPU in the GPU tests) gathers host tensors, so its device accumulators are staged through host
+    host = dist.get_backend(group) == "gloo"
 
     def ag(t):
-        parts = [torch.empty_like(t) for _ in range(W)]
-        dist.all_gather(parts, t.contiguous(), group=group)
-        return torch.cat(parts, dim=0)
+        src = t.contiguous().cpu() if host else t.contiguous()
+        parts = [torch.empty_like(src) for _ in range(W)]
+        dist.all_gather(parts, src, group=group)
+        return torch.cat(parts, dim=0).to(t.device)
 
-    S = torch.tensor([float(S_local)], dtype=torch.float64, device=m.device)
+    S = torch.tensor([float(S_local)], dtype=torch.float64, device="cpu" if host else m.device)
     dist.all_reduce(S, group=group)
     return ag(m), ag(s), (ag(e) if e is not None else None), float(S.item())

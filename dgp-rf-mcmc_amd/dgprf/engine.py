@@ -62,6 +62,17 @@ def next_subsequence():
     return s
 
 
+def engine_key():
+    """A fresh Philox key for a new Engine: the global seed mixed with the next subsequence
+    (splitmix64 finaliser), so two models built in one process draw independent step noise — as
+    the reference's tf.random.normal, whose global stream moves on between models
+    (models/dgp.py:210-212) — while staying reproducible under set_seed."""
+    x = (_RNG.seed + 0x9E3779B97F4A7C15 * (next_subsequence() + 1)) & 0xFFFFFFFFFFFFFFFF
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+    return x ^ (x >> 31)
+
+
 def normal(shape, purpose, dev=None, out=None):
     """N(0,1) tensor drawn on the device by dgprf_philox_normal."""
     dev = dev or device()
@@ -96,6 +107,8 @@ class ModelSpec:
 
 
 class Engine:
+    MAX_GRAPHS = 8  # instantiated step graphs kept per engine (LRU)
+
     def __init__(self, spec, n_chains=1, dev=None, seed=None, per_chain_hyp=None):
         """per_chain_hyp: every chain owns its kernel / likelihood hyper-parameters (and Omega),
         needed to sample them with full_bayesian=True across several chains; default: only when
@@ -122,10 +135,11 @@ class Engine:
         self.hmass = torch.ones(self.C, N.HMASS, dtype=_F32, device=self.dev)
         self.hyper_moments_ready = False
         self.step_ctr = torch.zeros(1, dtype=torch.int64, device=self.dev)
-        self.seed = _RNG.seed if seed is None else int(seed)
+        self.seed = engine_key() if seed is None else int(seed)
         self.lik_log_var_source = None  # callable -> device scalar tensor (Gaussian likelihood)
         self._ws = {}
         self._graphs = {}
+        self._fwd_scratch = None
         self.moments_ready = False
 
     # ---------------------------------------------------------------- views
@@ -334,11 +348,16 @@ class Engine:
         """hipGraph of `steps_per_graph` on-device-minibatched steps (DGPRF_BATCH_EPOCH)."""
         if full_bayes:
             self._check_full_bayes()
-        key = (X_all.data_ptr(), Y_all.data_ptr(), int(batch_size), float(data_size), float(lr),
-               float(beta), float(T), int(steps_per_graph), int(schedule), int(start_step),
-               int(cycle_length), bool(resample_head), int(perm_seed), bool(full_bayes))
+        key = (X_all.data_ptr(), tuple(X_all.shape), Y_all.data_ptr(), tuple(Y_all.shape),
+               int(batch_size), float(data_size), float(lr), float(beta), float(T),
+               int(steps_per_graph), int(schedule), int(start_step), int(cycle_length),
+               bool(resample_head), int(perm_seed), bool(full_bayes))
         if key in self._graphs:
-            return self._graphs[key]
+            g = self._graphs.pop(key)  # most recently used last
+            self._graphs[key] = g
+            return g
+        while len(self._graphs) >= self.MAX_GRAPHS:  # bounded: evict the least recently used
+            self._graphs.pop(next(iter(self._graphs)))
         pl, ws = self.plan_ws(batch_size)
         iters = X_all.shape[0] // int(batch_size)
         ch = self.chain_struct(ws)
@@ -348,7 +367,7 @@ class Engine:
         h = ctypes.c_void_p()
         N.call("dgprf_graph_create_sghmc", ctypes.byref(h), ctypes.byref(pl), ctypes.byref(ch),
                ctypes.byref(bt), ctypes.byref(st), int(steps_per_graph))
-        g = _Graph(h, (X_all, Y_all, ws))
+        g = _Graph(h, (X_all, Y_all, ws), int(steps_per_graph))
         self._graphs[key] = g
         return g
 
@@ -408,11 +427,30 @@ class Engine:
         if lse is not None:
             m, s, e = lse
         om = self.omega if omega is None else omega
+        scr = self.forward_scratch(n)
         N.call("dgprf_forward", ctypes.byref(self.layout), ptr(self.theta), ptr(om),
                ptr(self.der), ptr(X), ptr(Yd), int(y_cols), int(n), fptrs, ptr(lp), ptr(sq),
-               ptr(m), ptr(s), ptr(e), stream())
+               ptr(m), ptr(s), ptr(e), ptr(scr), 0 if scr is None else scr.numel(), stream())
         out["_keep"] = (X, Yd)
         return out
+
+    def forward_scratch(self, n):
+        """Engine-owned scratch of dgprf_forward for n rows (the wide-first-layer A_1 chunks),
+        grown on demand and reused, so the predictive loop allocates nothing per sample."""
+        need = ctypes.c_int64(0)
+        N.call("dgprf_forward_scratch", ctypes.byref(self.layout), int(n), ctypes.byref(need))
+        if need.value == 0:
+            return None
+        if self._fwd_scratch is None or self._fwd_scratch.numel() < need.value:
+            self._fwd_scratch = torch.empty(need.value, dtype=_F32, device=self.dev)
+        return self._fwd_scratch
+
+    def set_forward_path(self, path=N.FWD_AUTO, agemm_chunk_rows=0):
+        """Pin the predictive forward path (N.FWD_*) and the A_1 chunk size — parity tests of
+        each path; the product default is FWD_AUTO."""
+        self.layout.fwd_path = int(path)
+        self.layout.agemm_chunk_rows = int(agemm_chunk_rows)
+        N.call("dgprf_plan_init", ctypes.byref(self.layout))
 
     def prior_w(self):
         out = torch.empty(self.C, dtype=_F32, device=self.dev)
@@ -460,9 +498,10 @@ class Engine:
 
 
 class _Graph:
-    def __init__(self, handle, keep):
+    def __init__(self, handle, keep, steps=0):
         self.h = handle
         self._keep = keep
+        self.steps = steps  # SGHMC steps one replay runs
 
     def launch(self):
         N.call("dgprf_graph_launch", self.h, stream())

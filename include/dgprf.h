@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define DGPRF_ABI_VERSION 3
+#define DGPRF_ABI_VERSION 4
 
 #define DGPRF_MAX_LAYERS 8
 #define DGPRF_MAX_G 64        /* max latent GPs per layer (n_gp[l]) */
@@ -69,6 +69,13 @@ extern "C" {
  * reference's param.M). */
 #define DGPRF_HMASS 32
 
+/* predictive forward path (dgprf_plan_t.fwd_path).  AUTO is the product choice; the other two pin a
+ * path for parity tests: the general row kernel, or a wide first layer contracted inside the forward
+ * kernel instead of by the separate A_1 = X Omega_1 GEMM. */
+#define DGPRF_FWD_AUTO 0
+#define DGPRF_FWD_ROWS 1
+#define DGPRF_FWD_NO_AGEMM 2
+
 /* error codes */
 #define DGPRF_OK 0
 #define DGPRF_E_ARG -1         /* null pointer / bad scalar argument */
@@ -109,6 +116,9 @@ typedef struct dgprf_plan {
   int32_t hyp_flags;       /* DGPRF_HYP_* groups that are trainable (full_bayesian=True) */
   int32_t hyp_per_chain;   /* 1: hyp / omega / der are per chain ([C][...]); 0: shared */
   int32_t ard[DGPRF_MAX_LAYERS]; /* 1: per-dimension log_inv_ls; 0: one scalar (d equal slots) */
+  int32_t fwd_path;        /* DGPRF_FWD_* (0 = AUTO) */
+  int32_t agemm_chunk_rows; /* wide first layer: rows of A_1 per dgprf_forward chunk (0 = as many as
+                               fit 64M floats; otherwise rounded down to a multiple of 32, >= 32) */
   /* ---- derived by dgprf_plan_init ---- */
   int32_t initialised;
   int32_t d[DGPRF_MAX_LAYERS];      /* layer input width */
@@ -255,6 +265,10 @@ int dgprf_profile_step(const dgprf_plan_t *plan, const dgprf_chain_t *chain,
                        float *ms_out, void *stream);
 
 /* ---------------- predictive / forward ---------------- */
+/* Floats of device scratch dgprf_forward needs for n rows (0 unless the first layer is wide and the
+ * A_1 GEMM path is taken).  Host-only. */
+int dgprf_forward_scratch(const dgprf_plan_t *plan, int64_t n, int64_t *floats_out);
+
 /* Forward of n rows through all layers for every chain (BNN_from_list.__call__, utils.py:10-16;
  * BNN_from_list_input_cat.__call__, utils.py:32-44) plus the likelihood
  * (RegressionDGP.eval_log_likelihood_and_se, models/regression_model.py:33-50;
@@ -266,11 +280,12 @@ int dgprf_profile_step(const dgprf_plan_t *plan, const dgprf_chain_t *chain,
  *   lse_m/lse_s/se_sum [C][n]  online log-sum-exp over samples (experiments/utils_training.py:79-85)
  *                         updated in place: m' = max(m, lp); s' = s e^{m-m'} + e^{lp-m'}.
  * Y may be NULL when no likelihood output is requested.  omega/der are [C][...] when
- * plan.hyp_per_chain (chain c scored with its own hyper-parameters). */
+ * plan.hyp_per_chain (chain c scored with its own hyper-parameters).  scratch: >= the floats
+ * dgprf_forward_scratch reports for n (may be NULL when that is 0); owned by the caller. */
 int dgprf_forward(const dgprf_plan_t *plan, const float *theta, const float *omega,
                   const float *der, const float *X, const float *Y, int32_t y_cols, int64_t n,
                   float *const *f_out, float *logp, float *se, float *lse_m, float *lse_s,
-                  float *se_sum, void *stream);
+                  float *se_sum, float *scratch, int64_t scratch_floats, void *stream);
 
 /* Posterior-predictive summary (experiments/utils_training.py:79-85):
  * per point lse[n] = log sum_s exp(lp_s) over all chains' accumulators, and

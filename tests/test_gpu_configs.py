@@ -93,37 +93,6 @@ def test_config_forward_and_grad(dev, cfg):
         assert rel_err(G[l], ref[l]) < 2e-4, (cfg, l)
 
 
-@pytest.mark.parametrize("cfg", [3, 5])
-def test_config_sghmc_step_injected_noise(dev, cfg):
-    c = CONFIGS[cfg]
-    m, p = _model(c, 20 + cfg)
-    eng = m._engine
-    X, Y = _data(c, 2 * c["B"], 100 + cfg)
-    X, Y = _rows_off_kinks(c, p, X, Y, c["B"])
-    L = len(c["kinds"])
-    rng = np.random.default_rng(cfg)
-    m.precond_update(None, 1000, precond_type="identity")
-    m0 = [cpu(eng.mom_view(l)).astype(np.float64) for l in range(L)]
-    xi = [rng.standard_normal(w.shape) for w in p.W]
-    eng.step(X, Y, 1000, 0.01, 0.9, 1.0, xi=pack(eng, xi))
-    O.sgmcmc_step(p, m0, X, Y, 1000, 0.01, 0.9, 1.0, [1.0] * L, xi)
-    for l in range(L):
-        assert rel_err(cpu(eng.W_view(l)), p.W[l]) < 2e-5, (cfg, l)
-
-
-@pytest.mark.parametrize("cfg", [3, 4, 5])
-def test_config_predictive_rows(dev, cfg):
-    """eval_log_likelihood(_and_se) over a test set (tile kernel for configs 3 and 5, the general
-    row kernel for config 4's D = 784) against the oracle, row by row."""
-    c = CONFIGS[cfg]
-    m, p = _model(c, 30 + cfg)
-    Xt, Yt = _data(c, c["n_test"], 200 + cfg)
-    out = m._engine.forward(Xt, Yt, logp=True)
-    lp = cpu(out["logp"][0])
-    ref = O.log_prob(p, O.forward(p, Xt), Yt)
-    assert np.max(np.abs(lp - ref)) < 2e-5 * max(1.0, np.max(np.abs(ref)))
-
-
 def test_predictive_multi_round_rows(dev):
     """Config 2's shape (3-layer RBF, n_rf 1024, g [8,8,1]) over 70,001 test rows: more tiles than
     one round of resident waves (65,536 rows on 256 CUs) plus a ragged remainder; per-row log p
@@ -137,13 +106,16 @@ def test_predictive_multi_round_rows(dev):
     assert np.array_equal(lp, cpu(m._engine.forward(Xt, Yt, logp=True)["logp"][0]))
 
 
-@pytest.mark.parametrize("cfg", [3, 5])
+@pytest.mark.parametrize("cfg", [3, 4, 5])
 def test_config_sghmc_step_injected_noise(dev, cfg):
+    """One SGHMC step with injected noise at the config's full model shape; config 4 at its
+    benchmarked B = 200 (the A_1 GEMM step path, align32(B) = 224: ragged 32-row GEMM tiles)."""
     c = CONFIGS[cfg]
+    B = 200 if cfg == 4 else c["B"]
     m, p = _model(c, 20 + cfg)
     eng = m._engine
-    X, Y = _data(c, 2 * c["B"], 100 + cfg)
-    X, Y = _rows_off_kinks(c, p, X, Y, c["B"])
+    X, Y = _data(c, 2 * B, 100 + cfg)
+    X, Y = _rows_off_kinks(c, p, X, Y, B)
     L = len(c["kinds"])
     rng = np.random.default_rng(cfg)
     m.precond_update(None, 1000, precond_type="identity")
@@ -157,8 +129,9 @@ def test_config_sghmc_step_injected_noise(dev, cfg):
 
 @pytest.mark.parametrize("cfg", [3, 4, 5])
 def test_config_predictive_rows(dev, cfg):
-    """eval_log_likelihood(_and_se) over a test set (tile kernel for configs 3 and 5, the general
-    row kernel for config 4's D = 784) against the oracle, row by row."""
+    """eval_log_likelihood(_and_se) over a test set against the oracle, row by row (tile kernel for
+    every config; config 4's 784-wide first layer through the A_1 GEMM, read by the tile kernel's
+    WIDE layer 0)."""
     c = CONFIGS[cfg]
     m, p = _model(c, 30 + cfg)
     Xt, Yt = _data(c, c["n_test"], 200 + cfg)
@@ -168,36 +141,18 @@ def test_config_predictive_rows(dev, cfg):
     assert np.max(np.abs(lp - ref)) < 2e-5 * max(1.0, np.max(np.abs(ref)))
 
 
-@pytest.mark.parametrize("no_pair", [None, "1"])
-def test_predictive_tail_split_rows(dev, monkeypatch, no_pair):
-    """Config 2's shape (3-layer RBF, n_rf 1024, g [8,8,1]) over 70,001 test rows: one full round of
-    one-tile-per-wave tiles (65,536 rows on 256 CUs) plus a ragged remainder that runs as wave pairs
-    (default) or as single waves (DGPRF_TILE_NO_PAIR); per-row log p against the oracle, and the two
-    launch shapes bit-identical row by row."""
-    c = dict(kinds=["RBF"] * 3, n_rf=[1024] * 3, n_gp=[8, 8, 1], D=8, lik="gaussian")
-    m, p = _model(c, 61)
-    Xt, Yt = _data(c, 70_001, 62)
-    if no_pair:
-        monkeypatch.setenv("DGPRF_TILE_NO_PAIR", no_pair)
-    lp = cpu(m._engine.forward(Xt, Yt, logp=True)["logp"][0])
-    ref = O.log_prob(p, O.forward(p, Xt), Yt)
-    assert np.max(np.abs(lp - ref)) < 2e-5 * max(1.0, np.max(np.abs(ref)))
-    monkeypatch.setenv("DGPRF_TILE_NO_PAIR", "1")
-    lp1 = cpu(m._engine.forward(Xt, Yt, logp=True)["logp"][0])
-    monkeypatch.delenv("DGPRF_TILE_NO_PAIR")
-    lp2 = cpu(m._engine.forward(Xt, Yt, logp=True)["logp"][0])
-    assert np.array_equal(lp, lp1 if no_pair else lp2)
-    assert np.max(np.abs(lp1 - lp2)) < 2e-5 * max(1.0, np.max(np.abs(ref)))
-
-
-@pytest.mark.parametrize("cfg", [3, 5])
+@pytest.mark.parametrize("cfg", [3, 4, 5])
 def test_config_graph_steps_finite_and_deterministic(dev, cfg):
-    """200 graph-replayed steps with on-device minibatches at the config's N (config 5 scaled to
-    N = 2e5 rows to bound memory in the test): finite, and bit-identical on replay."""
+    """200 graph-replayed steps with on-device minibatches of B = 200 at the config's N (config 5
+    scaled to N = 2e5 rows to bound memory in the test): finite, and bit-identical on replay."""
     c = CONFIGS[cfg]
-    n = 45_730 if cfg == 3 else 200_000
-    X = torch.randn(n, c["D"], device=dev)
-    Y = torch.randn(n, 1, device=dev)
+    n = {3: 45_730, 4: 60_000, 5: 200_000}[cfg]
+    if c["lik"] == "softmax":
+        X = torch.rand(n, c["D"], device=dev) - 0.5
+        Y = torch.randint(0, c["n_gp"][-1], (n, 1), device=dev).float()
+    else:
+        X = torch.randn(n, c["D"], device=dev)
+        Y = torch.randn(n, 1, device=dev)
     out = []
     for _ in range(2):
         m, _ = _model(c, 40 + cfg)
@@ -208,17 +163,17 @@ def test_config_graph_steps_finite_and_deterministic(dev, cfg):
     assert torch.equal(out[0], out[1])
 
 
-@pytest.mark.parametrize("chunk_rows", [None, "64"])
-def test_wide_first_layer_forward_chunks(dev, monkeypatch, chunk_rows):
+@pytest.mark.parametrize("chunk_rows", [0, 64])
+def test_wide_first_layer_forward_chunks(dev, chunk_rows):
     """Wide first layer (d = 40 > 32): the A_1 GEMM + tile kernel, in one chunk and in 64-row chunks
-    (DGPRF_AGEMM_CHUNK_ROWS) over a ragged 201-row set, and through the row kernel; per-layer F and
-    the LSE accumulators against the oracle."""
+    (plan.agemm_chunk_rows) over a ragged 201-row set, through the row kernel (FWD_ROWS) and with
+    layer 0 contracted in-kernel (FWD_NO_AGEMM); per-layer F and the LSE accumulators against the
+    oracle."""
+    from dgprf import _native as N
     from dgprf import engine as E
     from dgprf.predictive import PredictiveLSE
     from likelihoods import Gaussian
     from models.dgp import DGP_RF
-    if chunk_rows:
-        monkeypatch.setenv("DGPRF_AGEMM_CHUNK_ROWS", chunk_rows)
     E.set_seed(51)
     kinds, n_rf, n_gp = ["RBF", "ARC", "RBF"], [96, 64, 48], [12, 6, 2]
     m = DGP_RF(40, 2, n_hidden_layers=3, n_rf=n_rf, n_gp=n_gp, likelihood=Gaussian(variance=0.2),
@@ -230,20 +185,19 @@ def test_wide_first_layer_forward_chunks(dev, monkeypatch, chunk_rows):
     rng = np.random.default_rng(8)
     X = rng.standard_normal((201, 40)).astype(np.float32).astype(np.float64)
     Y = rng.standard_normal((201, 2)).astype(np.float32).astype(np.float64)
-    for rows in (False, True):
-        if rows:
-            monkeypatch.setenv("DGPRF_FORWARD_ROWS", "1")
+    for path in (N.FWD_AUTO, N.FWD_ROWS, N.FWD_NO_AGEMM):
+        m._engine.set_forward_path(path, chunk_rows)
         outs = m._engine.forward(X, f_out="all")["F"]
         _, cache = O.forward(p, X, keep=True)
         for l in range(3):
-            assert rel_err(cpu(outs[l][0]), cache[l][2] @ p.W[l]) < 5e-5, (rows, l)
+            assert rel_err(cpu(outs[l][0]), cache[l][2] @ p.W[l]) < 5e-5, (path, l)
         acc = PredictiveLSE(m._engine, X, Y)
         acc.add_sample()
         ll, rmse = acc.finalize()
         lp, se = O.eval_log_likelihood_and_se(p, X, Y)
         ref_ll, ref_rmse = O.predictive_summary(lp[None], se[None])
         assert abs(ll - ref_ll) < 1e-4 and abs(rmse - ref_rmse) < 1e-5 * max(1.0, ref_rmse)
-    monkeypatch.delenv("DGPRF_FORWARD_ROWS")
+    m._engine.set_forward_path(N.FWD_AUTO)
 
 
 def test_wide_first_layer_full_bayes_grad(dev):

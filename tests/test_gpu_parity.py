@@ -512,3 +512,17 @@ def test_full_config2_properties(dev):
         runs.append(m._engine.theta.clone())
         assert torch.isfinite(runs[-1]).all()
     assert torch.equal(runs[0], runs[1])
+
+
+def test_softmax_label_outside_classes_is_nan(dev):
+    """int32(Y[:, 0]) outside [0, C) (likelihoods/softmax.py:14; TF raises on it) poisons log p
+    and the gradient with NaN instead of being scored as a clamped class."""
+    from likelihoods import Softmax
+    from models.dgp import DGP_RF
+    m = DGP_RF(3, 4, n_hidden_layers=1, n_rf=16, n_gp=4, likelihood=Softmax())
+    X = np.random.default_rng(0).standard_normal((5, 3)).astype(np.float32)
+    Y = np.array([[0], [3], [4], [-1], [2.7]], np.float32)
+    lp = cpu(m.log_likelihood(X, Y))
+    assert np.isfinite(lp[[0, 1, 4]]).all() and np.isnan(lp[[2, 3]]).all()
+    assert np.isnan(cpu(m._engine.grad(X, Y, 100))).any()
+    assert np.isfinite(cpu(m._engine.grad(X[[0, 1, 4]], Y[[0, 1, 4]], 100))).all()

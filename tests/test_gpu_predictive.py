@@ -1,0 +1,211 @@
+"""Posterior-predictive parity at BASELINE sizes: the HIP forward's online
+log-sum-exp folded over samples, chains and ranks, against the float64 oracle's
+experiments/utils_training.py:79-85 aggregation (oracle.predictive_summary) over the same samples.
+
+Tolerances (north_star): |dLL| < 1e-4 absolute; RMSE relative < 1e-5; per-point LSE |d| < 1e-4.
+The device path is the product one: hardware v_sin/v_cos after v_fract range reduction (the default
+build), one tile-kernel launch per sample with grid.y = C chains, k_lse_finalize over `parts`
+accumulator rows (chains x ranks).
+"""
+import math
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import dgp_oracle as O
+from test_gpu_parity import cpu, dev  # noqa: F401
+
+pytestmark = pytest.mark.gpu
+
+CFG2 = dict(kinds=["RBF"] * 3, n_rf=[1024] * 3, n_gp=[8, 8, 1], D=8, variance=0.1)
+
+
+def _config2_model(seed):
+    from dgprf import engine as E
+    from likelihoods import Gaussian
+    from models.regression_model import RegressionDGP
+    E.set_seed(seed)
+    return RegressionDGP(CFG2["D"], 1, n_hidden_layers=3, n_rf=CFG2["n_rf"], n_gp=CFG2["n_gp"],
+                         likelihood=Gaussian(variance=CFG2["variance"]))
+
+
+def _oracle_params(m, W):
+    """Oracle parameters of model m's kernels / frequencies with the GP weights W (list per layer)."""
+    L = m.n_hidden_layers
+    return O.Params(CFG2["D"], 1, CFG2["n_rf"], CFG2["n_gp"], CFG2["kinds"], "gaussian", False,
+                    z=[cpu(m.BNN.layers[2 * l].z) for l in range(L)], W=W,
+                    log_amp=[cpu(k.log_amplitude) for k in m.kernel_list],
+                    log_inv_ls=[cpu(k.log_inv_length_scale) for k in m.kernel_list],
+                    lik_log_var=np.log(CFG2["variance"]))
+
+
+def _unpack(eng, theta_row):
+    pl = eng.layout
+    return [np.asarray(theta_row[pl.w_off[l]:pl.w_off[l] + pl.P[l] * pl.n_gp[l]],
+                       dtype=np.float64).reshape(pl.P[l], pl.n_gp[l]) for l in range(eng.L)]
+
+
+def _oracle_lp_se(p, X, Y, chunk=10_000):
+    """Per-point log p and se of one sample, the oracle forward in row chunks (bounded memory)."""
+    lp, se = [], []
+    for i in range(0, X.shape[0], chunk):
+        a, b = O.eval_log_likelihood_and_se(p, X[i:i + chunk], Y[i:i + chunk])
+        lp.append(a)
+        se.append(b)
+    return np.concatenate(lp), np.concatenate(se)
+
+
+def _oracle_lse(lp, y_std=1.0):
+    l = np.asarray(lp, np.float64) - np.log(y_std)
+    mx = l.max(axis=0)
+    return mx + np.log(np.exp(l - mx).sum(axis=0))
+
+
+def test_predictive_ll_config2_70k_rows_4_samples(dev):
+    """Config 2's model (3 x RBF, n_rf 1024, g [8,8,1]) scored on N_t = 70,001 rows (one round of
+    resident tiles plus a ragged remainder) for S = 4 posterior samples drawn by graph-replayed
+    SGHMC on device-resident data: LL within 1e-4 and RMSE within 1e-5 relative of the oracle over
+    the same 4 samples, y_std = 1 and y_std = 1.7 (utils_training.py:63-64)."""
+    from dgprf.data import regression_data
+    from dgprf.predictive import PredictiveLSE
+    n_train, n_test = 100_000, 70_001
+    X, Y, a = regression_data(n_train, CFG2["D"], seed=0, device=dev)
+    Xt, Yt, _ = regression_data(n_test, CFG2["D"], seed=1, device=dev, a=a)
+    m = _config2_model(2)
+    m.precond_update(None, n_train, precond_type="identity")
+    acc = PredictiveLSE(m._engine, Xt, Yt)
+    Ws = []
+    for s in range(4):
+        m.run_sgmcmc(X, Y, n_train, 40, batch_size=200, lr=0.01, momentum_decay=0.9,
+                     steps_per_graph=20, perm_seed=3)
+        acc.add_sample()
+        Ws.append([cpu(w).astype(np.float64) for w in m.W_mcmc])
+    Xh, Yh = cpu(Xt).astype(np.float64), cpu(Yt).astype(np.float64)
+    lps, ses = zip(*[_oracle_lp_se(_oracle_params(m, W), Xh, Yh) for W in Ws])
+    for y_std in (1.0, 1.7):
+        ll, rmse = acc.finalize(y_std=y_std)
+        ref_ll, ref_rmse = O.predictive_summary(np.stack(lps), np.stack(ses), y_std=y_std)
+        assert abs(ll - ref_ll) < 1e-4, (y_std, ll, ref_ll)
+        assert abs(rmse - ref_rmse) < 1e-5 * ref_rmse, (y_std, rmse, ref_rmse)
+
+
+def _multi_chain_engine(m, C, seed):
+    """C chains sharing model m's frequencies and hyper-parameters (one posterior)."""
+    from dgprf import engine as E
+    eng = m._engine
+    me = E.Engine(eng.spec, C, seed=seed)
+    me.z.copy_(eng.z)
+    me.hyp.copy_(eng.hyp)
+    me.lik_log_var_source = eng.lik_log_var_source
+    me.build_omega()
+    return me
+
+
+def test_predictive_four_chains_and_eight_parts(dev):
+    """An engine with C = 4 chains (k_forward_tiles with grid.y = 4) folds 2 samples per chain
+    (finalize over parts = 4), and two such accumulator sets stacked as a two-rank gather
+    (k_lse_finalize over parts = 8, S = 16): LL, RMSE and the per-point LSE against the oracle over
+    all samples (utils_training.py:79-85 reduce_logsumexp over the stacked [S, N_t] matrix)."""
+    from dgprf import _native as N
+    from dgprf import engine as E
+    from dgprf.data import regression_data
+    from dgprf.predictive import PredictiveLSE
+    n_test = 20_001
+    Xt, Yt, _ = regression_data(n_test, CFG2["D"], seed=4, device=dev)
+    m = _config2_model(5)
+    me = _multi_chain_engine(m, 4, seed=77)
+    accs, thetas = [], []
+    E.set_seed(9)
+    for part in range(2):
+        acc = PredictiveLSE(me, Xt, Yt)
+        for s in range(2):
+            E.normal(None, N.RNG_W, out=me.theta)
+            thetas.append(cpu(me.theta))
+            acc.add_sample()
+        accs.append(acc)
+    Xh, Yh = cpu(Xt).astype(np.float64), cpu(Yt).astype(np.float64)
+    lp_all, se_all = [], []
+    for th in thetas:  # [4, w_total] per round
+        for c in range(4):
+            lp, se = _oracle_lp_se(_oracle_params(m, _unpack(me, th[c])), Xh, Yh)
+            lp_all.append(lp)
+            se_all.append(se)
+    lp_all, se_all = np.stack(lp_all), np.stack(se_all)
+    # one accumulator set: parts = 4 chains, 8 samples (rounds 0 and 1)
+    ll4, rmse4 = accs[0].finalize(y_std=1.0)
+    ref_ll4, ref_rmse4 = O.predictive_summary(lp_all[:8], se_all[:8])
+    assert abs(ll4 - ref_ll4) < 1e-4 and abs(rmse4 - ref_rmse4) < 1e-5 * ref_rmse4
+    # two sets stacked in rank order: parts = 8, S = 16
+    cat = lambda k: torch.cat([getattr(a, k) for a in accs], dim=0)
+    out, lse = E.lse_finalize(cat("m"), cat("s"), cat("e"), 16, y_std=2.0, lse_out=True)
+    out = out.cpu().numpy()
+    ref_ll8, ref_rmse8 = O.predictive_summary(lp_all, se_all, y_std=2.0)
+    assert abs(out[0] - ref_ll8) < 1e-4 and abs(out[1] - ref_rmse8) < 1e-5 * ref_rmse8
+    assert np.max(np.abs(cpu(lse) - _oracle_lse(lp_all, 2.0))) < 1e-4
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_worker(rank, world, port, q):
+    """One rank: 2 chains of its own (rank-keyed draws of W) over the shared test set and model,
+    2 samples each; PredictiveLSE.finalize all-gathers the accumulators (gloo: host-staged, two
+    ranks share the one GPU) and runs k_lse_finalize on the stacked [world * 2, n] rows."""
+    from dgprf import _native as N
+    from dgprf import engine as E
+    from dgprf.data import regression_data
+    from dgprf.distributed import rank_seed
+    from dgprf.predictive import PredictiveLSE
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    Xt, Yt, _ = regression_data(5_003, CFG2["D"], seed=6, device="cuda")
+    m = _config2_model(8)          # same frequencies / hyper-parameters on every rank
+    me = _multi_chain_engine(m, 2, seed=rank_seed(1, rank))
+    E.set_seed(rank_seed(2, rank))
+    acc = PredictiveLSE(me, Xt, Yt)
+    th = []
+    for s in range(2):
+        E.normal(None, N.RNG_W, out=me.theta)
+        th.append(cpu(me.theta))
+        acc.add_sample()
+    ll, rmse = acc.finalize(y_std=1.3)
+    q.put((rank, np.stack(th), ll, rmse))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_predictive_two_ranks_gather_and_finalize(dev):
+    """world_size 2 through PredictiveLSE.finalize (gather_accumulators + k_lse_finalize) on the
+    GPU: both ranks report the same LL / RMSE, equal to the oracle over all 8 samples."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    mp.spawn(_rank_worker, args=(world, port, q), nprocs=world, join=True)
+    res = sorted([q.get() for _ in range(world)], key=lambda r: r[0])
+    m = _config2_model(8)
+    from dgprf.data import regression_data
+    Xt, Yt, _ = regression_data(5_003, CFG2["D"], seed=6, device=dev)
+    Xh, Yh = cpu(Xt).astype(np.float64), cpu(Yt).astype(np.float64)
+    eng = m._engine
+    lp_all, se_all = [], []
+    for _, th, _, _ in res:                       # rank order, then sample, then chain
+        for s in range(th.shape[0]):
+            for c in range(th.shape[1]):
+                lp, se = _oracle_lp_se(_oracle_params(m, _unpack(eng, th[s, c])), Xh, Yh)
+                lp_all.append(lp)
+                se_all.append(se)
+    ref_ll, ref_rmse = O.predictive_summary(np.stack(lp_all), np.stack(se_all), y_std=1.3)
+    for _, _, ll, rmse in res:
+        assert abs(ll - ref_ll) < 1e-4 and abs(rmse - ref_rmse) < 1e-5 * ref_rmse
+    assert res[0][2] == res[1][2] and res[0][3] == res[1][3]
