@@ -921,10 +921,14 @@ ForwardCfg forward_cfg(const dgprf_plan_t& pl, int64_t n) {
   for (int l = 0; l < pl.n_layers; ++l)
     c.tiles = c.tiles && (pl.d[l] <= 32 || (l == 0 && c.wide0)) && pl.n_gp[l] <= 64 &&
               pl.n_rf[l] % 4 == 0 && (int64_t)2 * pl.n_rf[l] * pl.n_gp[l] < ((int64_t)1 << 29);
+  // chunks are whole 64-row tile-kernel workgroups: every wave of the last workgroup reads its 16
+  // A_1 rows (rows past n included, their outputs discarded), so the scratch covers align64 rows
   const int64_t R0 = pl.n_rf[0];
-  int64_t cap = (((int64_t)1 << 26) / R0) / 32 * 32;
-  if (pl.agemm_chunk_rows > 0) cap = std::max<int64_t>(32, pl.agemm_chunk_rows / 32 * 32);
-  c.chunk = c.wide0 ? std::max<int64_t>(32, std::min<int64_t>(cap, (n + 31) / 32 * 32)) : n;
+  int64_t cap = (((int64_t)1 << 26) / R0) / TW_ROWS * TW_ROWS;
+  if (pl.agemm_chunk_rows > 0)
+    cap = std::max<int64_t>(TW_ROWS, pl.agemm_chunk_rows / TW_ROWS * TW_ROWS);
+  c.chunk = c.wide0 ? std::max<int64_t>(TW_ROWS, std::min<int64_t>(cap, (n + TW_ROWS - 1) / TW_ROWS * TW_ROWS))
+                    : n;
   c.scratch_floats = c.wide0 && n > 0 ? c.chunk * R0 : 0;
   return c;
 }

@@ -146,6 +146,25 @@ def lib():
     return h
 
 
+TORCH_LIB_PATH = os.path.join(_HERE, "libdgprf_torch.so")
+_ops = None
+
+
+def torch_ops():
+    """Register the dgprf torch operators (libdgprf_torch.so: TORCH_LIBRARY(dgprf, m) over this
+    C-ABI) once and return torch.ops.dgprf.  Raises ImportError if it has not been built."""
+    global _ops
+    if _ops is None:
+        import torch
+        lib()  # libdgprf.so first (the op library links it)
+        if not os.path.exists(TORCH_LIB_PATH):
+            raise ImportError(f"libdgprf_torch.so not found at {TORCH_LIB_PATH}: build it with "
+                              "`make -C dgp-rf-mcmc_amd/csrc`. There is no CPU fallback.")
+        torch.ops.load_library(TORCH_LIB_PATH)
+        _ops = torch.ops.dgprf
+    return _ops
+
+
 def call(name, *args):
     """Call an entry point and raise DgprfError on a non-zero return code."""
     rc = getattr(lib(), name)(*args)

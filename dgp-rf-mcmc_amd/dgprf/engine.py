@@ -44,6 +44,18 @@ def as_device(x, dev, dtype=_F32):
     return x.to(device=dev, dtype=dtype).contiguous()
 
 
+def ops():
+    """torch.ops.dgprf — the hot-path entry points registered with torch's dispatcher
+    (libdgprf_torch.so over the C-ABI).  Raises if the extension is not built."""
+    return N.torch_ops()
+
+
+def _i64(u):
+    """A uint64 key / seed as the int64 a torch op schema carries (same bits)."""
+    u = int(u) & 0xFFFFFFFFFFFFFFFF
+    return u - (1 << 64) if u >= (1 << 63) else u
+
+
 # ------------------------------------------------------------------ global Philox stream state
 class _RNG:
     """Replacement of TF's global generator: key = seed, one fresh subsequence per draw."""
@@ -140,6 +152,7 @@ class Engine:
         self._ws = {}
         self._graphs = {}
         self._fwd_scratch = None
+        self._plan_tensors = {}
         self.moments_ready = False
 
     # ---------------------------------------------------------------- views
@@ -307,40 +320,55 @@ class Engine:
         if self.C > 1 and not self.per_chain_hyp:
             raise ValueError("full_bayesian=True with several chains needs per_chain_hyp=True")
 
+    def _plan_t(self, pl):
+        """The plan as the CPU uint8 tensor the torch ops take (cached per plan object)."""
+        t = self._plan_tensors.get(id(pl))
+        if t is None or t[0] is not pl:
+            t = (pl, torch.frombuffer(bytearray(bytes(pl)), dtype=torch.uint8))
+            self._plan_tensors[id(pl)] = t
+        return t[1]
+
+    def _op_batch(self, X, Y, batch_size, mode, idx, perm_seed):
+        X, Y = self._prep_batch(X, Y)
+        B = X.shape[0] if mode == N.BATCH_DIRECT else int(batch_size)
+        pl, ws = self.plan_ws(B)
+        if idx is not None:
+            idx = torch.as_tensor(idx).to(device=self.dev, dtype=torch.int32).contiguous()
+        iters = X.shape[0] // B if mode == N.BATCH_EPOCH else 0
+        return pl, ws, X, Y, idx, iters, _i64(perm_seed)
+
     def step(self, X, Y, data_size, lr, beta, T, resample=False, xi=None, xi_resample=None,
              build=True, omega=None, batch_size=None, mode=N.BATCH_DIRECT, idx=None,
              perm_seed=0, full_bayes=False, xi_hyp=None, xi_hyp_resample=None, z=None):
-        """One sgmcmc_update (default: X, Y are the batch, DGPRF_BATCH_DIRECT).
-        full_bayes: also update the trainable hyper-parameters (models/dgp.py:199-216); Omega,
-        c and sigma^2 are rebuilt on the device afterwards."""
+        """One sgmcmc_update (default: X, Y are the batch, DGPRF_BATCH_DIRECT) through the
+        dgprf::sghmc_step_ torch op.  full_bayes: also update the trainable hyper-parameters
+        (models/dgp.py:199-216); Omega, c and sigma^2 are rebuilt on the device afterwards."""
         if full_bayes:
             self._check_full_bayes()
-        pl, ws, bt, keep = self._batch(X, Y, batch_size, mode, idx, perm_seed)
+        pl, ws, X, Y, idx, iters, ps = self._op_batch(X, Y, batch_size, mode, idx, perm_seed)
         if build:
             self.build_omega()
-        ch = self.chain_struct(ws, omega, z)
         dv = lambda t: None if t is None else as_device(t, self.dev)
-        xi, xr, xh, xhr = dv(xi), dv(xi_resample), dv(xi_hyp), dv(xi_hyp_resample)
-        st = self.step_struct(lr, beta, T, data_size, resample, xi=xi, xi_resample=xr,
-                              full_bayes=full_bayes, xi_hyp=xh, xi_hyp_resample=xhr)
-        N.call("dgprf_sghmc_step", ctypes.byref(pl), ctypes.byref(ch), ctypes.byref(bt),
-               ctypes.byref(st), stream())
+        ops().sghmc_step_(
+            self._plan_t(pl), self.theta, self.mom, self.omega if omega is None else omega,
+            self.der, self.mass, ws, self.step_ctr, _i64(self.seed), X, Y, int(mode), iters, ps,
+            idx, float(lr), float(beta), float(T), float(data_size), bool(resample), dv(xi),
+            dv(xi_resample), bool(full_bayes), self.z if z is None else z, self.hyp, self.hmom,
+            self.hmass, dv(xi_hyp), dv(xi_hyp_resample))
 
     def grad(self, X, Y, data_size, build=True, omega=None, batch_size=None,
              mode=N.BATCH_DIRECT, idx=None, perm_seed=0, full_bayes=False, z=None):
-        """dU/dW for every layer and chain -> [C, w_total] (dgprf_potential_grad); full_bayes:
+        """dU/dW for every layer and chain -> [C, w_total] (dgprf::potential_grad); full_bayes:
         w.r.t. every trainable variable -> [C, w_total + hyp_total] (hyp layout after W)."""
         if full_bayes and self.C > 1 and not self.per_chain_hyp:
             raise ValueError("full_bayesian=True with several chains needs per_chain_hyp=True")
-        pl, ws, bt, keep = self._batch(X, Y, batch_size, mode, idx, perm_seed)
+        pl, ws, X, Y, idx, iters, ps = self._op_batch(X, Y, batch_size, mode, idx, perm_seed)
         if build:
             self.build_omega()
-        n = self.layout.w_total + (self.layout.hyp_total if full_bayes else 0)
-        out = torch.empty(self.C, n, dtype=_F32, device=self.dev)
-        ch = self.chain_struct(ws, omega, z)
-        N.call("dgprf_potential_grad", ctypes.byref(pl), ctypes.byref(ch), ctypes.byref(bt),
-               float(data_size), int(bool(full_bayes)), ptr(out), stream())
-        return out
+        return ops().potential_grad(
+            self._plan_t(pl), self.theta, self.omega if omega is None else omega, self.der,
+            self.mass, ws, self.step_ctr, X, Y, int(mode), iters, ps, idx, float(data_size),
+            bool(full_bayes), self.z if z is None else z, self.hyp, self.hmom, self.hmass)
 
     def graph(self, X_all, Y_all, batch_size, data_size, lr, beta, T, steps_per_graph,
               schedule=N.SCHED_CONST, start_step=0, cycle_length=1, resample_head=False,
@@ -401,37 +429,29 @@ class Engine:
             raise ValueError(f"X must be [n, {self.spec.d_in}], got {tuple(X.shape)}")
         if build:
             self.build_omega()
-        out = {}
-        fptrs = (ctypes.c_void_p * N.MAX_LAYERS)()
+        mask = 0
         if f_out:
-            Fs = []
             for l in range(self.L):
                 if f_out == "all" or l == self.L - 1:
-                    t = torch.empty(self.C, n, self.layout.n_gp[l], dtype=_F32, device=self.dev)
-                    fptrs[l] = t.data_ptr()
-                    Fs.append(t)
-            out["F"] = Fs
-        y_cols, Yd = 0, None
+                    mask |= 1 << l
+        Yd = None
         if Y is not None:
             Yd = as_device(Y, self.dev)
             if Yd.dim() == 1:
                 Yd = Yd[:, None]
-            y_cols = Yd.shape[1]
-        lp = torch.empty(self.C, n, dtype=_F32, device=self.dev) if logp else None
-        sq = torch.empty(self.C, n, dtype=_F32, device=self.dev) if se else None
-        if lp is not None:
-            out["logp"] = lp
-        if sq is not None:
-            out["se"] = sq
         m = s = e = None
         if lse is not None:
             m, s, e = lse
         om = self.omega if omega is None else omega
-        scr = self.forward_scratch(n)
-        N.call("dgprf_forward", ctypes.byref(self.layout), ptr(self.theta), ptr(om),
-               ptr(self.der), ptr(X), ptr(Yd), int(y_cols), int(n), fptrs, ptr(lp), ptr(sq),
-               ptr(m), ptr(s), ptr(e), ptr(scr), 0 if scr is None else scr.numel(), stream())
-        out["_keep"] = (X, Yd)
+        Fs, lp, sq = ops().forward(self._plan_t(self.layout), self.theta, om, self.der, X, Yd,
+                                   mask, bool(logp), bool(se), m, s, e, self.forward_scratch(n))
+        out = {}
+        if f_out:
+            out["F"] = list(Fs)
+        if logp:
+            out["logp"] = lp
+        if se:
+            out["se"] = sq
         return out
 
     def forward_scratch(self, n):
@@ -451,6 +471,7 @@ class Engine:
         self.layout.fwd_path = int(path)
         self.layout.agemm_chunk_rows = int(agemm_chunk_rows)
         N.call("dgprf_plan_init", ctypes.byref(self.layout))
+        self._plan_tensors.pop(id(self.layout), None)
 
     def prior_w(self):
         out = torch.empty(self.C, dtype=_F32, device=self.dev)
@@ -515,10 +536,9 @@ class _Graph:
 
 
 def lse_finalize(lse_m, lse_s, se_sum, s_total, y_std=1.0, lse_out=False):
-    """Posterior-predictive LL / RMSE from stacked accumulators [parts, n] (dgprf_lse_finalize)."""
-    parts, n = lse_m.shape
-    out = torch.zeros(2, dtype=torch.float64, device=lse_m.device)
-    lo = torch.empty(n, dtype=_F32, device=lse_m.device) if lse_out else None
-    N.call("dgprf_lse_finalize", ptr(lse_m), ptr(lse_s), ptr(se_sum), int(parts), int(n),
-           float(s_total), float(math.log(y_std)), float(y_std), ptr(lo), ptr(out), stream())
-    return out, lo
+    """Posterior-predictive LL / RMSE from stacked accumulators [parts, n] (dgprf::lse_finalize):
+    returns (float64 [LL, RMSE] on the device, per-point LSE [n] or None)."""
+    out, lo = ops().lse_finalize(lse_m.contiguous(), lse_s.contiguous(),
+                                 None if se_sum is None else se_sum.contiguous(), float(s_total),
+                                 float(y_std), bool(lse_out))
+    return out, (lo if lse_out else None)

@@ -118,7 +118,7 @@ typedef struct dgprf_plan {
   int32_t ard[DGPRF_MAX_LAYERS]; /* 1: per-dimension log_inv_ls; 0: one scalar (d equal slots) */
   int32_t fwd_path;        /* DGPRF_FWD_* (0 = AUTO) */
   int32_t agemm_chunk_rows; /* wide first layer: rows of A_1 per dgprf_forward chunk (0 = as many as
-                               fit 64M floats; otherwise rounded down to a multiple of 32, >= 32) */
+                               fit 64M floats; otherwise rounded down to a multiple of 64, >= 64) */
   /* ---- derived by dgprf_plan_init ---- */
   int32_t initialised;
   int32_t d[DGPRF_MAX_LAYERS];      /* layer input width */
