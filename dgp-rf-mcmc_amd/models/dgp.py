@@ -410,7 +410,6 @@ class DGP_RF(Module):
                                   momentum_decay, temperature, steps_per_graph, perm_seed,
                                   schedule, start_step, cycle_length, resample_in_cycle_head,
                                   full_bayesian)
-        self._engine.build_omega()
         for g, reps in plan:
             for _ in range(reps):
                 g.launch()
@@ -422,7 +421,9 @@ class DGP_RF(Module):
         """The hipGraphs run_sgmcmc replays for these arguments, as [(graph, replays)]: a graph of
         spg = min(steps_per_graph, n_steps) steps replayed n_steps // spg times, then one graph of
         the remaining n_steps % spg steps.  Graphs are cached on the engine, so a caller that
-        times run_sgmcmc captures them here first and the timed call only replays."""
+        times run_sgmcmc captures them here first and the timed call only replays.  Omega, c and
+        sigma^2 are built from the current hyper-parameters, so the graphs can be launched as they
+        are returned."""
         self._check_moments(full_bayesian)
         eng = self._engine
         if not all(self.BNN.layers[2 * l].random_fixed for l in range(self.n_hidden_layers)):
@@ -436,6 +437,7 @@ class DGP_RF(Module):
         mk = lambda k: eng.graph(X_all, Y_all, batch_size, data_size, lr, momentum_decay,
                                  temperature, k, sched, start_step, cycle_length,
                                  resample_in_cycle_head, perm_seed, full_bayes=bool(full_bayesian))
+        eng.build_omega()
         full, rest = divmod(int(n_steps), spg)
         plan = [(mk(spg), full)] if full else []
         if rest:

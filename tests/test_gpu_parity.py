@@ -235,6 +235,7 @@ def test_device_philox_noise_counter(dev, golden):
     g = golden("mixed5")
     a, b = model_from_fixture(g), model_from_fixture(g)
     lr, beta, T, N_ = g["step_scalars"]
+    b._engine.seed = a._engine.seed  # each model draws its own key (engine_key): share a's here
     for mm in (a, b):
         mm.precond_update(None, N_, precond_type="identity")
         mm._engine.mom.zero_()
@@ -246,6 +247,32 @@ def test_device_philox_noise_counter(dev, golden):
              xi=torch.as_tensor(xi, dtype=torch.float32)[None])
     assert rel_err(cpu(a._engine.theta), cpu(eng.theta)) < 1e-5
     assert int(a._engine.step_ctr) == 6
+
+
+def test_two_models_draw_independent_noise(dev):
+    """Two models built in one process get distinct Philox keys (the reference's global
+    tf.random.normal stream moves on between models, models/dgp.py:210-212): from identical state
+    and data their SGHMC steps differ; set_seed makes the keys reproducible."""
+    from dgprf import engine as E
+    from likelihoods import Gaussian
+    from models.regression_model import RegressionDGP
+    mk = lambda: RegressionDGP(3, 1, n_hidden_layers=2, n_rf=16, n_gp=[2, 1],
+                               likelihood=Gaussian(variance=0.1))
+    E.set_seed(11)
+    a, b = mk(), mk()
+    E.set_seed(11)
+    c = mk()
+    assert a._engine.seed != b._engine.seed and c._engine.seed == a._engine.seed
+    rng = np.random.default_rng(0)
+    X = rng.standard_normal((20, 3)).astype(np.float32)
+    Y = rng.standard_normal((20, 1)).astype(np.float32)
+    for mm in (a, b):
+        mm.precond_update(None, 100, precond_type="identity")
+    for t in ("z", "theta", "mom", "hyp"):
+        getattr(b._engine, t).copy_(getattr(a._engine, t))
+    a.sgmcmc_update(X, Y, 100, lr=0.01)
+    b.sgmcmc_update(X, Y, 100, lr=0.01)
+    assert not torch.equal(a._engine.theta, b._engine.theta)
 
 
 # ----------------------------------------------------------------------------- minibatching

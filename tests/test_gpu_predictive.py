@@ -146,7 +146,10 @@ def test_predictive_four_chains_and_eight_parts(dev):
     out = out.cpu().numpy()
     ref_ll8, ref_rmse8 = O.predictive_summary(lp_all, se_all, y_std=2.0)
     assert abs(out[0] - ref_ll8) < 1e-4 and abs(out[1] - ref_rmse8) < 1e-5 * ref_rmse8
-    assert np.max(np.abs(cpu(lse) - _oracle_lse(lp_all, 2.0))) < 1e-4
+    # per point: 2e-5 of the point's |LSE| (random N(0,1) weights put |log p| in the hundreds for
+    # some points, where one fp32 ulp of log p is already ~3e-5); the 1e-4 bound is on the mean
+    ref_lse = _oracle_lse(lp_all)  # lse_out is LSE_s log p (no y_std shift, include/dgprf.h)
+    assert np.all(np.abs(cpu(lse) - ref_lse) < 2e-5 * np.maximum(1.0, np.abs(ref_lse)))
 
 
 def _free_port():
@@ -191,8 +194,10 @@ def test_predictive_two_ranks_gather_and_finalize(dev):
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    mp.spawn(_rank_worker, args=(world, port, q), nprocs=world, join=True)
-    res = sorted([q.get() for _ in range(world)], key=lambda r: r[0])
+    procs = mp.spawn(_rank_worker, args=(world, port, q), nprocs=world, join=False)
+    # drain the queue before joining: a child cannot exit while its queued arrays sit in the pipe
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda r: r[0])
+    procs.join()
     m = _config2_model(8)
     from dgprf.data import regression_data
     Xt, Yt, _ = regression_data(5_003, CFG2["D"], seed=6, device=dev)
