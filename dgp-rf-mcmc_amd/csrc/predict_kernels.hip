@@ -367,16 +367,50 @@ __global__ __launch_bounds__(256) void k_rf_features(const int kind, const float
   }
 }
 
-// F = Phi W (layers/GP_weight_layers.py:13); one thread per output element.
-__global__ void k_gp_matmul(const float* __restrict__ phi, const int64_t n, const int P,
-                            const float* __restrict__ W, const int g, float* __restrict__ F) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n * g) return;
-  const int64_t b = i / g;
-  const int o = (int)(i - b * g);
-  float acc = 0.f;
-  for (int k = 0; k < P; ++k) acc = fmaf(phi[b * P + k], W[(int64_t)k * g + o], acc);
-  F[i] = acc;
+// F = Phi W (layers/GP_weight_layers.py:11-15, the stand-alone GPLayer.__call__) on MFMA: a
+// 256-thread workgroup owns a 16-row x 16-output tile of F; its 4 waves split K = P into 16-wide
+// blocks (wave w takes blocks w, w + 4, ...), each block four v_mfma_f32_16x16x4_f32 with lane
+// (lr, lq) holding Phi[row lr][k0 + 4lq .. +3] as one 16-byte load and W[k0 + 4lq + s][o lr];
+// the four K-partial tiles are summed in LDS in wave order (deterministic).  Rows >= n, k >= P
+// and outputs >= g read 0 through the buffer descriptors (no traffic) and are never stored.
+__global__ __launch_bounds__(256) void k_gp_matmul(const float* __restrict__ phi, const int64_t n,
+                                                   const int P, const float* __restrict__ W,
+                                                   const int g, float* __restrict__ F) {
+  __shared__ __attribute__((aligned(16))) float red[4][16][17];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, lr = lane & 15, lq = lane >> 4;
+  const int64_t row0 = (int64_t)blockIdx.x * 16;
+  const int o0 = (int)blockIdx.y * 16;
+  const int64_t rows = min((int64_t)16, n - row0);
+  const rsrc_t rp = make_rsrc(phi + row0 * P, rows * P);
+  const rsrc_t rw = make_rsrc(W, (int64_t)P * g);
+  const bool rok = lr < rows, ook = o0 + lr < g;
+  const bool vec = (P & 3) == 0;  // 16-byte aligned Phi rows
+  f4 acc = f4zero();
+  const int nkb = (P + 15) >> 4;
+  for (int kb = wave; kb < nkb; kb += 4) {
+    const int k = kb * 16 + 4 * lq;
+    f4 a;
+    if (vec) {
+      a = bload4(rp, rok && k < P ? (uint32_t)(((int64_t)lr * P + k) * 4) : DGPRF_OOB);
+    } else {
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        a[s] = bload1(rp, rok && k + s < P ? (uint32_t)(((int64_t)lr * P + k + s) * 4) : DGPRF_OOB);
+    }
+    float b[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      b[s] = bload1(rw, ook && k + s < P ? (uint32_t)(((int64_t)(k + s) * g + o0 + lr) * 4) : DGPRF_OOB);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc = mfma16(a[s], b[s], acc);
+  }
+  // acc[r] = partial F[row0 + 4lq + r][o0 + lr]
+#pragma unroll
+  for (int r = 0; r < 4; ++r) red[wave][4 * lq + r][lr] = acc[r];
+  __syncthreads();
+  const int i = threadIdx.x >> 4, j = threadIdx.x & 15;
+  if (i < rows && o0 + j < g)
+    F[(row0 + i) * g + o0 + j] = ((red[0][i][j] + red[1][i][j]) + red[2][i][j]) + red[3][i][j];
 }
 
 // sum_l sum log N(W_l; 0, 1) per chain (models/dgp.py:129-136), fixed-order tree reduction.
@@ -1049,10 +1083,12 @@ hipError_t launch_rf_features(int kind, const float* X, int64_t n, int d, const 
 
 hipError_t launch_gp_matmul(const float* phi, int64_t n, int P, const float* W, int g, float* F,
                             hipStream_t s) {
-  const int64_t tot = n * g;
-  if (tot <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_gp_matmul, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, phi, n, P,
-                     W, g, F);
+  if (n <= 0) return hipSuccess;
+  // 32-bit buffer offsets within one 16-row tile of Phi and within W
+  if ((int64_t)16 * P >= ((int64_t)1 << 29) || (int64_t)P * g >= ((int64_t)1 << 29))
+    return hipErrorInvalidValue;
+  dim3 grid((unsigned)((n + 15) / 16), (unsigned)((g + 15) / 16));
+  hipLaunchKernelGGL(k_gp_matmul, grid, dim3(256), 0, s, phi, n, P, W, g, F);
   return hipGetLastError();
 }
 

@@ -70,14 +70,43 @@ struct LayerK {
   float* hp;            // hyper partials [n_rt_pad][NSM][round4(2d+1)] of chain 0 (stride ws_cs)
   float* hpl;           // lik_log_var partials [n_rt_pad] (last layer)
   int32_t hred_off, lik_fb;
+  // fused SGHMC update (plan.fused_update, W-only steps; models/dgp.py:206-216)
+  float* th0;           // theta of chain 0 (chain stride w_cs)
+  float* mo0;           // momenta of chain 0 (chain stride w_cs)
+  const float* mass;    // [C][L]
+  const int64_t* step;
+  const float* gwb;     // gW partial rows of chain 0 (ws + gwp_off; row stride w_cs, chain ws_cs)
+  unsigned* tick;       // W_1 slice arrival tickets of chain 0 (ws + tick_off, chain stride ws_cs)
+  uint64_t seed;
+  int32_t pend;         // forward, layer 0: apply the previous step's pending W_1 update first
+  int32_t pend_lo;      // w_off of layer 0
+  int32_t smap, pad_s;  // slice-major block map (tile_of_block)
+  int32_t main_blocks;  // this layer's (row tile, slice) workgroups; extra workgroups follow
+  int32_t upd_blocks, upd_layer, upd_lo, upd_hi;  // backward extras: the update of layer upd_layer's
+                                                  // W (packed range [upd_lo, upd_hi))
+  int32_t gat_blocks, n_layers, upd_t_off, gat_t_off;
+  UpdateDev ud;
+  BatchDev bd;          // backward extras of the last layer: rows of step t+1 ...
+  float* xb_next;       // ... into the other gathered-rows buffer (chain stride ws_cs)
+  float* yb_next;
+  int32_t yb_cols, pad_f;
 };
 
 // Block -> (row tile, slice): blocks are dealt round-robin over the 8 XCDs, so block b's XCD group
 // is b % 8; every workgroup of row tile rt gets group rt % 8, so the slice partials it exchanges
 // with the neighbouring layers' kernels stay within one L2.  Speed only: correctness never depends
 // on placement.  Blocks past the last row tile exit at once.
+// Slice-major map (a.smap, the forward applying the pending W_1 update): every row tile of slice sl
+// runs on XCD sl % 8 instead, so the 13 workgroups that each sum the slice's gW partials read them
+// through one L2.
 __device__ __forceinline__ bool tile_of_block(const LayerK& a, int& rt, int& sl) {
   const int b = blockIdx.x, grp = b & 7, idx = b >> 3;
+  if (a.smap) {
+    const int k = idx / a.n_rt;
+    rt = idx - k * a.n_rt;
+    sl = grp + 8 * k;
+    return sl < a.ns;
+  }
   const int j = idx / a.ns;
   sl = idx - j * a.ns;
   rt = grp + 8 * j;
@@ -336,13 +365,220 @@ __device__ __forceinline__ void load_w_frag(const float* __restrict__ W, int R, 
     }
   }
 }
+// The same fragments from the forward's LDS copy of the freshly updated W_1 slice (PEND):
+// pw[h][(f - fb0) g + o], nhalf floats per half.
+template <int NOT, bool RBF, bool G1>
+__device__ __forceinline__ void load_w_frag_lds(const float* pw, int nhalf, int R, int g, int fb0,
+                                                int f0, int lr, int lq, float (&wf)[NOT][4][2]) {
+#pragma unroll
+  for (int ot = 0; ot < NOT; ++ot) {
+    const int oc = G1 ? 0 : min(ot * 16 + lr, g - 1);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int fl = min(f0 + 4 * lq + r, R - 1) - fb0;
+      wf[ot][r][0] = pw[fl * g + oc];
+      wf[ot][r][1] = RBF ? pw[nhalf + fl * g + oc] : 0.f;
+    }
+  }
+}
 template <bool G1>
 __device__ __forceinline__ bool w_ok(int ot, int r, int R, int g, int f0, int lr, int lq) {
   return (G1 || ot * 16 + lr < g) && f0 + 4 * lq + r < R;
 }
 
+// ------------------------------------------------------------------------- update / gather
+__device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
+__device__ __forceinline__ void st4(float* p, f4 v) { *reinterpret_cast<f4*>(p) = v; }
+
+// cyclical_step_rate (utils.py:49-73) with min_value = 0 as used by the drivers
+// (experiments/utils_training.py:53-54): lr = lr0 * rate^2.
+__device__ __forceinline__ float cyclical_rate(int64_t step_index, int64_t cycle) {
+  const float frac = (float)((step_index - 1) % cycle) / (float)cycle;
+  return 0.0f + (1.0f - 0.0f) * 0.5f * (cosf(3.14159265358979f * frac) + 1.0f);
+}
+
+// Copy minibatch row b of chain `chain` at step t into the gathered-rows workspace.
+__device__ __forceinline__ void gather_row(const BatchDev& bd, int B, int d_in, int yb_cols,
+                                           float* xb, float* yb, int chain, int64_t t, int b) {
+  const int64_t row = batch_row(bd, B, chain, t, b);
+  const float* xs = bd.X + row * d_in;
+  const float* ys = bd.Y + row * bd.y_cols;
+  float* xd = xb + (int64_t)b * d_in;
+  float* yd = yb + (int64_t)b * yb_cols;
+  for (int k = 0; k < d_in; ++k) xd[k] = xs[k];
+  for (int k = 0; k < yb_cols; ++k) yd[k] = ys[k];
+}
+
+// Wide rows (d_in > GATHER_WIDE, e.g. 784 MNIST pixels): one 64-lane wave per row, lanes striding
+// over the columns (coalesced, all loads issued before the stores) instead of one thread per row.
+constexpr int GATHER_WIDE = 16;
+__device__ __forceinline__ void gather_row_wave(const BatchDev& bd, int B, int d_in, int yb_cols,
+                                                float* xb, float* yb, int chain, int64_t t, int b,
+                                                int lane) {
+  const int64_t row = batch_row(bd, B, chain, t, b);
+  const float* xs = bd.X + row * d_in;
+  float* xd = xb + (int64_t)b * d_in;
+  constexpr int U = 8;
+  for (int k0 = 0; k0 < d_in; k0 += 64 * U) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = k0 + 64 * u + lane;
+      v[u] = k < d_in ? xs[k] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = k0 + 64 * u + lane;
+      if (k < d_in) xd[k] = v[u];
+    }
+  }
+  for (int k = lane; k < yb_cols; k += 64) yb[(int64_t)b * yb_cols + k] = bd.Y[row * bd.y_cols + k];
+}
+
+// Schedule of step t (utils.py:49-73 via experiments/utils_training.py:41-61 when CYC).
+template <bool CYC>
+__device__ __forceinline__ void step_schedule(const UpdateDev& ud, int64_t t, float* lr, float* T,
+                                              int* resample) {
+  *lr = ud.lr;
+  *T = ud.temperature;
+  *resample = ud.resample;
+  if (CYC) {
+    if (t < ud.start_step) {  // burn-in: fixed lr, zero temperature
+      *T = 0.f;
+      *resample = 0;
+    } else {
+      const int64_t si = t - ud.start_step + 1;
+      const float rate = cyclical_rate(si, ud.cycle_length);
+      *lr = ud.lr * (rate * rate);
+      *T = 1.f;
+      *resample = ud.resample_head && (si % ud.cycle_length == 1);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------- fused update
+// The SGHMC / SGLD update of models/dgp.py:206-216 for W-only steps, run inside the step kernels
+// (plan.fused_update): 4 consecutive packed elements e0..e0+3 (e0 % 4 == 0) of chain `chain`.
+//   g = W / N + sum_rt gW_rt   (prior N(0,1), models/dgp.py:129-136,171; row-tile partials in order)
+//   m <- b m - h N g + sqrt(2 (1 - b) T M) xi,   W <- W + (h / M) m,   h = sqrt(lr / N)
+// with the noise xi (and resampled m) the Philox stream (seed, sub = t, purpose, tag = chain) at
+// counter quad e0 / 4 — the same values, in the same arithmetic order, as k_step_update.
+__device__ __forceinline__ void step_schedule_rt(const UpdateDev& ud, int64_t t, float* lr, float* T,
+                                                 int* resample) {
+  if (ud.schedule == DGPRF_SCHED_CYCLICAL) step_schedule<true>(ud, t, lr, T, resample);
+  else step_schedule<false>(ud, t, lr, T, resample);
+}
+
+struct UpdScal {
+  float N, h, beta, T;
+  int resample;
+};
+__device__ __forceinline__ UpdScal upd_scalars(const UpdateDev& ud, int64_t t) {
+  UpdScal u;
+  float lr;
+  step_schedule_rt(ud, t, &lr, &u.T, &u.resample);
+  u.N = ud.data_size;
+  u.h = sqrtf(lr / u.N);
+  u.beta = ud.beta;
+  return u;
+}
+
+__device__ __forceinline__ void sghmc4(const UpdateDev& ud, const UpdScal& u, float M, uint64_t seed,
+                                       int64_t t, int chain, int64_t cw, int64_t e0, f4 th, f4 m,
+                                       f4 gl, f4* th_new, f4* m_new) {
+  const f4 gr = th / u.N + gl;
+  const uint32_t quad = (uint32_t)(e0 >> 2);
+  if (u.resample) {  // models/dgp.py:209-210 (ignores M, Appendix A.1)
+    if (ud.xi_resample) {
+      m = *reinterpret_cast<const f4*>(ud.xi_resample + cw + e0);
+    } else {
+      m = philox_normal4(seed, (uint64_t)t, DGPRF_RNG_RESAMPLE, (uint32_t)chain, quad);
+    }
+  }
+  f4 mn = u.beta * m - (u.h * u.N) * gr;
+  const f4 eps = ud.xi ? *reinterpret_cast<const f4*>(ud.xi + cw + e0)
+                       : philox_normal4(seed, (uint64_t)t, DGPRF_RNG_NOISE, (uint32_t)chain, quad);
+  mn = mn + sqrtf(2.0f * (1.0f - u.beta) * u.T * M) * eps;
+  *m_new = mn;
+  *th_new = th + (u.h * (1.0f / M)) * mn;
+}
+
+// Sum of the row-tile gW partials of element quad e0 (n_rt <= NSM rows, fixed order from row 0;
+// rows past n_rt lie outside the descriptor: 0, no memory access).
+__device__ __forceinline__ f4 gw_partial_sum(rsrc_t rs, int64_t row_stride, int n_rt, int64_t e0,
+                                             bool ok = true) {
+  // rows past n_rt (wave-uniform) are not issued at all; masked lanes read 0 without traffic
+  f4 v[NSM];
+#pragma unroll
+  for (int rt = 0; rt < NSM; ++rt)
+    v[rt] = rt < n_rt ? bload4(rs, ok ? (uint32_t)((rt * row_stride + e0) * 4) : DGPRF_OOB) : f4zero();
+  f4 acc = f4zero();
+#pragma unroll
+  for (int rt = 0; rt < NSM; ++rt) acc += v[rt];
+  return acc;
+}
+
+// ------------------------------------------------------------------------- fused update workgroups
+// One 256-thread workgroup's 1024 packed elements of the update of layer a.upd_layer's W from its
+// row-tile gW partials (written by an earlier kernel): extra workgroups of the next layer's
+// backward, or the flush kernel.
+__device__ __forceinline__ void update_layer_block(const LayerK& a, int j, int chain) {
+  const int64_t e0 = a.upd_lo + 4 * ((int64_t)j * 256 + threadIdx.x);
+  if (e0 >= a.upd_hi) return;
+  const int64_t cw = (int64_t)chain * a.w_cs;
+  const f4 th = *reinterpret_cast<const f4*>(a.th0 + cw + e0);
+  const f4 m = *reinterpret_cast<const f4*>(a.mo0 + cw + e0);
+  const rsrc_t rs = make_rsrc(a.gwb + (int64_t)chain * a.ws_cs, (int64_t)a.n_rt * a.w_cs);
+  const f4 gl = gw_partial_sum(rs, a.w_cs, a.n_rt, e0);
+  const float M = a.mass[chain * a.n_layers + a.upd_layer];
+  // the step counter is read after the parameter and partial loads are in flight
+  const int64_t t = *a.step + a.upd_t_off;
+  const UpdScal u = upd_scalars(a.ud, t);
+  f4 thn, mn;
+  sghmc4(a.ud, u, M, a.seed, t, chain, cw, e0, th, m, gl, &thn, &mn);
+  if (e0 + 3 < a.upd_hi) {
+    st4(a.mo0 + cw + e0, mn);
+    st4(a.th0 + cw + e0, thn);
+  } else {  // layer padding between align4 offsets stays untouched
+    for (int i = 0; i < 4 && e0 + i < a.upd_hi; ++i) {
+      a.mo0[cw + e0 + i] = mn[i];
+      a.th0[cw + e0 + i] = thn[i];
+    }
+  }
+}
+
+// Extra workgroup j of a backward: the W update first, then the gather of step t+1's rows.
+__device__ __forceinline__ void bwd_extra_block(const LayerK& a, int j, int chain) {
+  if (j < a.upd_blocks) {
+    update_layer_block(a, j, chain);
+    return;
+  }
+  j -= a.upd_blocks;
+  const int64_t t = *a.step + a.gat_t_off;
+  float* xb = a.xb_next + (int64_t)chain * a.ws_cs;
+  float* yb = a.yb_next + (int64_t)chain * a.ws_cs;
+  if (a.d_in > GATHER_WIDE) {  // one wave per row
+    const int b = j * 4 + (int)(threadIdx.x >> 6);
+    if (b < a.B) gather_row_wave(a.bd, a.B, a.d_in, a.yb_cols, xb, yb, chain, t, b, threadIdx.x & 63);
+    return;
+  }
+  const int b = j * 256 + (int)threadIdx.x;
+  if (b < a.B) gather_row(a.bd, a.B, a.d_in, a.yb_cols, xb, yb, chain, t, b);
+}
+
+__global__ __launch_bounds__(256) void k_layer_update(const LayerK a) {
+  update_layer_block(a, (int)blockIdx.x, (int)blockIdx.z);
+}
+
 // ------------------------------------------------------------------------- forward
-template <int KS, int NOT, bool RBF, bool G1>
+// PEND (layer 0, fused update): the workgroup first applies the previous step's pending update to
+// its feature slice of W_1 (both halves: theta, momenta and the 13 row-tile gW partials loaded
+// alongside the X tile), keeps the new slice in LDS for its W fragments, and takes an arrival
+// ticket; the slice's last workgroup to arrive stores the new theta / momenta at its end — every
+// other workgroup of the slice has read the old values by then (its ticket follows its loads), so
+// no workgroup can see a half-updated slice.  Every workgroup of the slice computes bit-identical
+// values (same inputs, same order, same Philox counters).
+template <int KS, int NOT, bool RBF, bool G1, bool PEND>
 // Minimum waves per SIMD the register allocation must allow.  Single-chain steps run one workgroup
 // per CU either way; with C chains per launch (13 x 16 x C workgroups) residency sets throughput:
 // the g <= 16, d <= 8 W-only backward at <= 168 VGPRs (3 waves/SIMD) measured 127k -> 156k
@@ -368,10 +604,35 @@ __global__ __launch_bounds__(256) void k_step_fwd(const LayerK a) {
   const float* __restrict__ W = a.W + (int64_t)chain * a.w_cs;
   auto chunk_f0 = [&](int i) { return ((sl * cpw + i) * NW + wave) * 16; };
 
+  // PEND: old theta / momenta / gW partials of the slice, issued first (up to 4 quads per thread)
+  constexpr int PQ = PEND ? 4 : 1;
+  const int nfs = 64 * cpw, fb0 = sl * nfs, nhalf = nfs * g;
+  const int nvq = max(min(nfs, R - fb0), 0) * g / 4;  // valid quads per half (R g % 4 == 0)
+  const int nhq = nhalf / 4, nq = (RBF ? 2 : 1) * nhq;
+  const int64_t cw = (int64_t)chain * a.w_cs;
+  float* pw = smem + a.stg_off;  // new W_1 slice [h][nhalf]; flag word at pw[8192 / 2]
+  f4 pth[PQ], pmo[PQ], pgl[PQ];
+  int64_t t_pend = 0;
+  if (PEND) {
+    t_pend = *a.step;  // the step counter's round trip overlaps the loads below
+    const rsrc_t rth = make_rsrc(a.th0 + cw, a.w_cs), rmo = make_rsrc(a.mo0 + cw, a.w_cs);
+    const rsrc_t rs = make_rsrc(a.gwb + (int64_t)chain * a.ws_cs, (int64_t)a.n_rt * a.w_cs);
+#pragma unroll
+    for (int j = 0; j < PQ; ++j) {
+      pth[j] = pmo[j] = pgl[j] = f4zero();
+      if (256 * j >= nq) continue;  // wave-uniform: nothing issued for empty rounds
+      const int q = (int)threadIdx.x + 256 * j, h = q >= nhq ? 1 : 0, ql = q - h * nhq;
+      const bool ok = q < nq && ql < nvq;
+      const int64_t e0 = a.pend_lo + (int64_t)(h * R + fb0) * g + 4 * ql;
+      pth[j] = bload4(rth, ok ? (uint32_t)(e0 * 4) : DGPRF_OOB);
+      pmo[j] = bload4(rmo, ok ? (uint32_t)(e0 * 4) : DGPRF_OOB);
+      pgl[j] = gw_partial_sum(rs, a.w_cs, a.n_rt, e0, ok);
+    }
+  }
   // first chunk's fragments: independent of the X tile, issued first
   float omk[8], wf[NOT][4][2];
   if (KS > 0) load_om_frag<KS>(om, R, d, chunk_f0(0), lr, lq, omk);
-  load_w_frag<NOT, RBF, G1>(W, R, g, chunk_f0(0), lr, lq, wf);
+  if (!PEND) load_w_frag<NOT, RBF, G1>(W, R, g, chunk_f0(0), lr, lq, wf);
   const float cl = a.cptr[(int64_t)chain * a.der_cs];
   DGPRF_STAMP(stamp_base, 1);
   if (a.fast) {
@@ -379,9 +640,33 @@ __global__ __launch_bounds__(256) void k_step_fwd(const LayerK a) {
   } else if (KS > 0 || !a.a0) {
     load_x_tile(a, chain, row0, xs);
   }
+  if (PEND) {
+    const int64_t t = t_pend + a.upd_t_off;
+    const UpdScal u = upd_scalars(a.ud, t);
+    const float M = a.mass[chain * a.n_layers];
+#pragma unroll
+    for (int j = 0; j < PQ; ++j) {
+      const int q = (int)threadIdx.x + 256 * j, h = q >= nhq ? 1 : 0, ql = q - h * nhq;
+      if (q < nq) {
+        const bool ok = ql < nvq;
+        const int64_t e0 = a.pend_lo + (int64_t)(h * R + fb0) * g + 4 * ql;
+        f4 thn = f4zero(), mn = f4zero();
+        if (ok) sghmc4(a.ud, u, M, a.seed, t, chain, cw, e0, pth[j], pmo[j], pgl[j], &thn, &mn);
+        pth[j] = thn;
+        pmo[j] = mn;
+        *reinterpret_cast<f4*>(pw + h * nhalf + 4 * ql) = thn;  // features >= R stage as zeros
+      }
+    }
+  }
   const float* a0 = KS == 0 && a.a0 ? a.a0 + (int64_t)chain * a.ws_cs + (int64_t)(row0 + lr) * R : nullptr;
   __syncthreads();
   DGPRF_STAMP(stamp_base, 2);
+  unsigned ticket = 0u;
+  if (PEND) {
+    // every thread's old values are in registers (the barrier follows their use): arrive
+    if (threadIdx.x == 0) ticket = atomicAdd(a.tick + (int64_t)chain * a.ws_cs + 32 * sl, 1u);
+    load_w_frag_lds<NOT, RBF, G1>(pw, nhalf, R, g, fb0, chunk_f0(0), lr, lq, wf);
+  }
 
   float xf[8];
 #pragma unroll
@@ -410,7 +695,8 @@ __global__ __launch_bounds__(256) void k_step_fwd(const LayerK a) {
       }
     if (i + 1 < cpw) {  // prefetch the next chunk (clamped loads are always in range)
       if (KS > 0) load_om_frag<KS>(om, R, d, chunk_f0(i + 1), lr, lq, omk);
-      load_w_frag<NOT, RBF, G1>(W, R, g, chunk_f0(i + 1), lr, lq, wf);
+      if (PEND) load_w_frag_lds<NOT, RBF, G1>(pw, nhalf, R, g, fb0, chunk_f0(i + 1), lr, lq, wf);
+      else load_w_frag<NOT, RBF, G1>(W, R, g, chunk_f0(i + 1), lr, lq, wf);
     }
     if (G1) {
       // g == 1: F[row lr] += sum_f Phi[lr][f] W[f], 4 features per lane (VALU)
@@ -444,6 +730,7 @@ __global__ __launch_bounds__(256) void k_step_fwd(const LayerK a) {
       for (int r = 0; r < 4; ++r) redw[lr * GP + ot * 16 + 4 * lq + r] = acc[ot][r] + acs[ot][r];
   }
   DGPRF_STAMP(stamp_base, 3);
+  if (PEND && threadIdx.x == 0) pw[4096] = ticket == (unsigned)a.n_rt - 1u ? 1.f : 0.f;
   __syncthreads();
   float* fp = a.fout + (int64_t)chain * a.ws_cs + (int64_t)sl * B * g;
   for (int e = threadIdx.x; e < TR * g; e += blockDim.x) {
@@ -455,6 +742,18 @@ __global__ __launch_bounds__(256) void k_step_fwd(const LayerK a) {
       fp[(int64_t)b * g + o] = v;
     }
   }
+  if (PEND && pw[4096] != 0.f) {  // the slice's last arrival: store the new W_1 slice
+#pragma unroll
+    for (int j = 0; j < PQ; ++j) {
+      const int q = (int)threadIdx.x + 256 * j, h = q >= nhq ? 1 : 0, ql = q - h * nhq;
+      if (q < nq && ql < nvq) {
+        const int64_t e0 = a.pend_lo + (int64_t)(h * R + fb0) * g + 4 * ql;
+        st4(a.mo0 + cw + e0, pmo[j]);
+        st4(a.th0 + cw + e0, pth[j]);
+      }
+    }
+    if (threadIdx.x == 0) atomicExch(a.tick + (int64_t)chain * a.ws_cs + 32 * sl, 0u);  // next launch
+  }
 #ifdef DGPRF_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
@@ -465,6 +764,10 @@ __global__ __launch_bounds__(256) void k_step_fwd(const LayerK a) {
 template <int KS, int NOT, bool RBF, bool G1, bool FB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NOT == 1 && !FB && (KS == 1 || KS == 2 || (KS == 4 && !RBF))) ? DGPRF_STEP_WPE : 1))) void k_step_bwd(const LayerK a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  if ((int)blockIdx.x >= a.main_blocks) {  // fused update of W_{l+2} / next-batch gather
+    bwd_extra_block(a, (int)blockIdx.x - a.main_blocks, (int)blockIdx.z);
+    return;
+  }
   int rt, sl;
   if (!tile_of_block(a, rt, sl)) return;
   const int chain = blockIdx.z;
@@ -883,55 +1186,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NOT == 1 &
   DGPRF_STAMP(stamp_base, 14);
 }
 
-// ------------------------------------------------------------------------- update / gather
-__device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
-__device__ __forceinline__ void st4(float* p, f4 v) { *reinterpret_cast<f4*>(p) = v; }
-
-// cyclical_step_rate (utils.py:49-73) with min_value = 0 as used by the drivers
-// (experiments/utils_training.py:53-54): lr = lr0 * rate^2.
-__device__ __forceinline__ float cyclical_rate(int64_t step_index, int64_t cycle) {
-  const float frac = (float)((step_index - 1) % cycle) / (float)cycle;
-  return 0.0f + (1.0f - 0.0f) * 0.5f * (cosf(3.14159265358979f * frac) + 1.0f);
-}
-
-// Copy minibatch row b of chain `chain` at step t into the gathered-rows workspace.
-__device__ __forceinline__ void gather_row(const BatchDev& bd, int B, int d_in, int yb_cols,
-                                           float* xb, float* yb, int chain, int64_t t, int b) {
-  const int64_t row = batch_row(bd, B, chain, t, b);
-  const float* xs = bd.X + row * d_in;
-  const float* ys = bd.Y + row * bd.y_cols;
-  float* xd = xb + (int64_t)b * d_in;
-  float* yd = yb + (int64_t)b * yb_cols;
-  for (int k = 0; k < d_in; ++k) xd[k] = xs[k];
-  for (int k = 0; k < yb_cols; ++k) yd[k] = ys[k];
-}
-
-// Wide rows (d_in > GATHER_WIDE, e.g. 784 MNIST pixels): one 64-lane wave per row, lanes striding
-// over the columns (coalesced, all loads issued before the stores) instead of one thread per row.
-constexpr int GATHER_WIDE = 16;
-__device__ __forceinline__ void gather_row_wave(const BatchDev& bd, int B, int d_in, int yb_cols,
-                                                float* xb, float* yb, int chain, int64_t t, int b,
-                                                int lane) {
-  const int64_t row = batch_row(bd, B, chain, t, b);
-  const float* xs = bd.X + row * d_in;
-  float* xd = xb + (int64_t)b * d_in;
-  constexpr int U = 8;
-  for (int k0 = 0; k0 < d_in; k0 += 64 * U) {
-    float v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int k = k0 + 64 * u + lane;
-      v[u] = k < d_in ? xs[k] : 0.f;
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int k = k0 + 64 * u + lane;
-      if (k < d_in) xd[k] = v[u];
-    }
-  }
-  for (int k = lane; k < yb_cols; k += 64) yb[(int64_t)b * yb_cols + k] = bd.Y[row * bd.y_cols + k];
-}
-
 struct GatherK {
   BatchDev bd;
   const int64_t* step;
@@ -983,27 +1237,6 @@ __device__ __forceinline__ void st2(float* p, f2 v) { *reinterpret_cast<f2*>(p) 
 constexpr int UPD_THREADS = 64;
 __device__ __forceinline__ f2 bload2(rsrc_t r, uint32_t byte_off) {
   return __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(r, byte_off, 0, 0));
-}
-
-// Schedule of step t (utils.py:49-73 via experiments/utils_training.py:41-61 when CYC).
-template <bool CYC>
-__device__ __forceinline__ void step_schedule(const UpdateDev& ud, int64_t t, float* lr, float* T,
-                                              int* resample) {
-  *lr = ud.lr;
-  *T = ud.temperature;
-  *resample = ud.resample;
-  if (CYC) {
-    if (t < ud.start_step) {  // burn-in: fixed lr, zero temperature
-      *T = 0.f;
-      *resample = 0;
-    } else {
-      const int64_t si = t - ud.start_step + 1;
-      const float rate = cyclical_rate(si, ud.cycle_length);
-      *lr = ud.lr * (rate * rate);
-      *T = 1.f;
-      *resample = ud.resample_head && (si % ud.cycle_length == 1);
-    }
-  }
 }
 
 // One N(0,1) of the hyper-parameter streams (not inlined: the hyper path runs once per step on
@@ -1471,8 +1704,8 @@ LayerK make_layer_k(const dgprf_plan_t& pl, const StepDev& sd, int l, int& lds_f
   a.dxout = l > 0 ? sd.ws + pl.dxp_off[l] : sd.ws;
   a.gwp = sd.ws + pl.gwp_off + pl.w_off[l];
   a.logp = sd.ws + pl.logp_off;
-  a.xrows = direct ? sd.bd.X : sd.ws + pl.xb_off;
-  a.yrows = direct ? sd.bd.Y : sd.ws + pl.yb_off;
+  a.xrows = direct ? sd.bd.X : sd.ws + (sd.xb_sel ? pl.xb_alt_off : pl.xb_off);
+  a.yrows = direct ? sd.bd.Y : sd.ws + (sd.xb_sel ? pl.yb_alt_off : pl.yb_off);
   a.xrow_cs = direct ? 0 : pl.ws_chain;
   a.yrow_cs = direct ? 0 : pl.ws_chain;
   a.y_cols = direct ? sd.bd.y_cols : pl.yb_cols;
@@ -1514,7 +1747,43 @@ LayerK make_layer_k(const dgprf_plan_t& pl, const StepDev& sd, int l, int& lds_f
   a.lik_fb = (pl.hyp_flags & DGPRF_HYP_LIK) != 0 && pl.likelihood == DGPRF_LIK_GAUSSIAN;
   a.hred_off = lds_floats;
   if (sd.full_bayes) lds_floats += NW * round4(2 * a.d + 1);
+  // fused update: off unless the launcher sets it up (fill_fused)
+  a.main_blocks = 8 * a.rt_per_xcd * a.ns;
+  a.smap = a.pad_s = 0;
+  a.pend = a.upd_blocks = a.gat_blocks = 0;
+  a.th0 = a.mo0 = nullptr;
+  a.mass = nullptr;
+  a.step = sd.step;
+  a.gwb = nullptr;
+  a.tick = nullptr;
+  a.seed = sd.seed;
+  a.n_layers = pl.n_layers;
+  a.pend_lo = a.upd_layer = a.upd_lo = a.upd_hi = a.upd_t_off = a.gat_t_off = 0;
+  std::memset(&a.ud, 0, sizeof(a.ud));
+  std::memset(&a.bd, 0, sizeof(a.bd));
+  a.xb_next = a.yb_next = nullptr;
+  a.yb_cols = pl.yb_cols;
+  a.pad_f = 0;
   return a;
+}
+
+// The state the fused-update paths of a layer launch read (plan.fused_update).
+void fill_fused(LayerK& a, const dgprf_plan_t& pl, const StepDev& sd, const UpdateDev& ud) {
+  a.th0 = sd.theta;
+  a.mo0 = sd.mom;
+  a.mass = sd.mass;
+  a.gwb = sd.ws + pl.gwp_off;
+  a.tick = reinterpret_cast<unsigned*>(sd.ws + pl.tick_off);
+  a.ud = ud;
+}
+
+// Layer `layer`'s packed W range for the update workgroups.
+void set_update_range(LayerK& a, const dgprf_plan_t& pl, int layer, int t_off) {
+  a.upd_layer = layer;
+  a.upd_lo = (int32_t)pl.w_off[layer];
+  a.upd_hi = (int32_t)(pl.w_off[layer] + (int64_t)pl.P[layer] * pl.n_gp[layer]);
+  a.upd_blocks = (a.upd_hi - a.upd_lo + 1023) / 1024;
+  a.upd_t_off = t_off;
 }
 
 #define DGPRF_KS_NOT_DISPATCH(KERNEL)                                                              \
@@ -1549,7 +1818,41 @@ LayerK make_layer_k(const dgprf_plan_t& pl, const StepDev& sd, int l, int& lds_f
     else KERNEL##_launch2<0>(g, rbf, grid, lds, s, a);                                             \
   }
 
-DGPRF_KS_NOT_DISPATCH(k_step_fwd)
+// forward: KS x NOT x RBF x G1 (x PEND for the narrow layers the fused update covers: NOT == 1)
+template <int KS, int NOT, bool G1>
+void k_step_fwd_launch3(bool rbf, bool pend, dim3 grid, size_t lds, hipStream_t s, const LayerK& a) {
+#define DGPRF_FWD(R_, P_)                                                              \
+  do {                                                                                \
+    dgprf::set_lds_limit((const void*)k_step_fwd<KS, NOT, R_, G1, P_>, lds);         \
+    hipLaunchKernelGGL((k_step_fwd<KS, NOT, R_, G1, P_>), grid, dim3(256), lds, s, a); \
+  } while (0)
+  if (pend && NOT == 1) {
+    if (rbf) DGPRF_FWD(true, NOT == 1);
+    else DGPRF_FWD(false, NOT == 1);
+  } else {
+    if (rbf) DGPRF_FWD(true, false);
+    else DGPRF_FWD(false, false);
+  }
+#undef DGPRF_FWD
+}
+template <int KS>
+void k_step_fwd_launch2(int g, bool rbf, bool pend, dim3 grid, size_t lds, hipStream_t s,
+                        const LayerK& a) {
+  const int NOT = (g + 15) >> 4;
+  if (g == 1) k_step_fwd_launch3<KS, 1, true>(rbf, pend, grid, lds, s, a);
+  else if (NOT == 1) k_step_fwd_launch3<KS, 1, false>(rbf, pend, grid, lds, s, a);
+  else if (NOT == 2) k_step_fwd_launch3<KS, 2, false>(rbf, false, grid, lds, s, a);
+  else if (NOT == 3) k_step_fwd_launch3<KS, 3, false>(rbf, false, grid, lds, s, a);
+  else k_step_fwd_launch3<KS, 4, false>(rbf, false, grid, lds, s, a);
+}
+void k_step_fwd_launch(int d, int g, bool rbf, bool pend, dim3 grid, size_t lds, hipStream_t s,
+                       const LayerK& a) {
+  if (d <= 4) k_step_fwd_launch2<1>(g, rbf, pend, grid, lds, s, a);
+  else if (d <= 8) k_step_fwd_launch2<2>(g, rbf, pend, grid, lds, s, a);
+  else if (d <= 16) k_step_fwd_launch2<4>(g, rbf, pend, grid, lds, s, a);
+  else if (d <= 32) k_step_fwd_launch2<8>(g, rbf, pend, grid, lds, s, a);
+  else k_step_fwd_launch2<0>(g, rbf, false, grid, lds, s, a);
+}
 
 // backward: KS x NOT x RBF x G1 x FB
 template <int KS, int NOT, bool G1>
@@ -1604,9 +1907,20 @@ extern "C" int dgprf_debug_clear_stamps(void) {
 
 namespace dgprf {
 
-hipError_t launch_step_fwd(const dgprf_plan_t& pl, const StepDev& sd, int layer, hipStream_t s) {
+hipError_t launch_step_fwd(const dgprf_plan_t& pl, const StepDev& sd, int layer, hipStream_t s,
+                           const UpdateDev* ud, bool pend) {
   int lds_floats = 0;
-  const LayerK a = make_layer_k(pl, sd, layer, lds_floats);
+  LayerK a = make_layer_k(pl, sd, layer, lds_floats);
+  pend = pend && ud && layer == 0 && pl.fused_update && pl.n_gp[0] <= 16 && pl.d[0] <= 32;
+  if (pend) {  // the previous step's W_1 update, applied by this forward (its step offset - 1)
+    fill_fused(a, pl, sd, *ud);
+    a.pend = 1;
+    a.pend_lo = (int32_t)pl.w_off[0];
+    a.upd_t_off = sd.step_offset - 1;
+    lds_floats = max(lds_floats, a.stg_off + 4096 + 4);  // the new slice + the last-arrival flag
+    a.smap = 1;
+    a.main_blocks = 8 * ((a.ns + 7) / 8) * a.n_rt;
+  }
   if (a.a0) {  // wide first layer: A_1 = X Omega_1 first (k_step_agemm)
     AgemmK g;
     g.xrows = a.xrows;
@@ -1622,19 +1936,43 @@ hipError_t launch_step_fwd(const dgprf_plan_t& pl, const StepDev& sd, int layer,
     dim3 ggrid((unsigned)((g.R + 63) / 64), (unsigned)((g.B + 31) / 32), pl.n_chains);
     hipLaunchKernelGGL(k_step_agemm, ggrid, dim3(256), 0, s, g);
   }
-  dim3 grid(8 * a.rt_per_xcd * a.ns, 1, pl.n_chains);
-  k_step_fwd_launch(pl.d[layer], pl.n_gp[layer], pl.kind[layer] == DGPRF_RBF, grid,
+  dim3 grid(a.main_blocks, 1, pl.n_chains);
+  k_step_fwd_launch(pl.d[layer], pl.n_gp[layer], pl.kind[layer] == DGPRF_RBF, pend, grid,
                     (size_t)lds_floats * sizeof(float), s, a);
   return hipGetLastError();
 }
 
-hipError_t launch_step_bwd(const dgprf_plan_t& pl, const StepDev& sd, int layer, hipStream_t s) {
+hipError_t launch_step_bwd(const dgprf_plan_t& pl, const StepDev& sd, int layer, hipStream_t s,
+                           const UpdateDev* ud, bool gather_next) {
   int lds_floats = 0;
-  const LayerK a = make_layer_k(pl, sd, layer, lds_floats);
-  dim3 grid(8 * a.rt_per_xcd * a.ns, 1, pl.n_chains);
+  LayerK a = make_layer_k(pl, sd, layer, lds_floats);
+  if (ud && pl.fused_update) {
+    fill_fused(a, pl, sd, *ud);
+    // extra workgroups: W_{l+2}'s update from the gW partials layer l+1's backward just wrote
+    if (layer + 1 < pl.n_layers) set_update_range(a, pl, layer + 1, sd.step_offset);
+    // and, in the last layer's backward, step t+1's rows into the other buffer
+    if (gather_next && layer == pl.n_layers - 1 && sd.bd.mode == DGPRF_BATCH_EPOCH) {
+      a.gat_blocks = pl.d_in > GATHER_WIDE ? (pl.batch + 3) / 4 : (pl.batch + 255) / 256;
+      a.bd = sd.bd;
+      a.xb_next = sd.ws + (sd.xb_sel ? pl.xb_off : pl.xb_alt_off);
+      a.yb_next = sd.ws + (sd.xb_sel ? pl.yb_off : pl.yb_alt_off);
+      a.gat_t_off = sd.step_offset + 1;
+    }
+  }
+  dim3 grid(a.main_blocks + a.upd_blocks + a.gat_blocks, 1, pl.n_chains);
   k_step_bwd_launch(pl.d[layer], pl.n_gp[layer], pl.kind[layer] == DGPRF_RBF, sd.full_bayes != 0,
                     grid,
                     (size_t)lds_floats * sizeof(float), s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_layer_update(const dgprf_plan_t& pl, const StepDev& sd, const UpdateDev& ud,
+                               int layer, hipStream_t s) {
+  int lds_floats = 0;
+  LayerK a = make_layer_k(pl, sd, layer, lds_floats);
+  fill_fused(a, pl, sd, ud);
+  set_update_range(a, pl, layer, sd.step_offset);
+  hipLaunchKernelGGL(k_layer_update, dim3(a.upd_blocks, 1, pl.n_chains), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
@@ -1772,8 +2110,8 @@ hipError_t launch_gather(const dgprf_plan_t& pl, const StepDev& sd, hipStream_t 
   GatherK a;
   a.bd = sd.bd;
   a.step = sd.step;
-  a.xb = sd.ws + pl.xb_off;
-  a.yb = sd.ws + pl.yb_off;
+  a.xb = sd.ws + (sd.xb_sel ? pl.xb_alt_off : pl.xb_off);
+  a.yb = sd.ws + (sd.xb_sel ? pl.yb_alt_off : pl.yb_off);
   a.ws_cs = pl.ws_chain;
   a.B = pl.batch;
   a.d_in = pl.d_in;

@@ -120,6 +120,10 @@ class ModelSpec:
 
 class Engine:
     MAX_GRAPHS = 8  # instantiated step graphs kept per engine (LRU)
+    # request plan.fuse_update (set before the first step of a batch size): the SGHMC update inside
+    # the forward / backward kernels instead of one update kernel per step — correct, but measured
+    # no faster on config 2 and slower on config 3 / many chains, so off by default
+    fused_update = False
 
     def __init__(self, spec, n_chains=1, dev=None, seed=None, per_chain_hyp=None):
         """per_chain_hyp: every chain owns its kernel / likelihood hyper-parameters (and Omega),
@@ -226,6 +230,9 @@ class Engine:
         B = int(B)
         if B not in self._ws:
             pl = self.spec.plan(B, self.C, self.per_chain_hyp)
+            if self.fused_update:  # request the fused W-only update (plan_init grants or not)
+                pl.fuse_update = 1
+                N.call("dgprf_plan_init", ctypes.byref(pl))
             ws = torch.zeros(max(pl.ws_total, 4), dtype=_F32, device=self.dev)
             self._ws[B] = (pl, ws)
         return self._ws[B]

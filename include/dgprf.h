@@ -119,6 +119,8 @@ typedef struct dgprf_plan {
   int32_t fwd_path;        /* DGPRF_FWD_* (0 = AUTO) */
   int32_t agemm_chunk_rows; /* wide first layer: rows of A_1 per dgprf_forward chunk (0 = as many as
                                fit 64M floats; otherwise rounded down to a multiple of 64, >= 64) */
+  int32_t fuse_update;     /* 1: request the fused W-only update (see fused_update below) */
+  int32_t pad_c;
   /* ---- derived by dgprf_plan_init ---- */
   int32_t initialised;
   int32_t d[DGPRF_MAX_LAYERS];      /* layer input width */
@@ -147,10 +149,21 @@ typedef struct dgprf_plan {
   int64_t xb_off;                    /* gathered minibatch rows X [B][d_in] (per chain)        */
   int64_t yb_off;                    /* gathered minibatch targets [B][yb_cols] (per chain)    */
   int32_t yb_cols;                   /* g_L (Gaussian) or 1 (softmax label)                    */
-  int32_t pad2;
+  int32_t fused_update;              /* fuse_update granted (the shapes allow it; measured no
+                                        faster on config 2, DESIGN.md §4, so off by default).
+                                        1: W-only steps apply the SGHMC update inside the forward
+                                        / backward kernels (no separate update launch): W_{l+1} by
+                                        extra workgroups of layer l's backward, W_1 deferred into the
+                                        next step's layer-1 forward (or a flush kernel at the end of
+                                        a call / graph).  0: the update kernel runs per step.     */
   int64_t a0_off;                    /* layer 1 with d > 32 (e.g. the 784-wide MNIST input):
                                         A_1 = X Omega_1 [align32(B)][R_1] precomputed by one tiled
                                         MFMA GEMM per step (per chain); -1 when not used          */
+  int64_t xb_alt_off;                /* second gathered-rows buffers (graph steps alternate      */
+  int64_t yb_alt_off;                /*   between the two by step parity)                       */
+  int64_t tick_off;                  /* [16][32] uint32 arrival tickets of the deferred W_1
+                                        update, one 128-byte line per feature slice (per chain;
+                                        zero between launches)                                   */
 } dgprf_plan_t;
 
 /* Device state of the chains.  Replaces the tf.Variables W and their ad-hoc attributes

@@ -1,0 +1,44 @@
+"""Diagnostic: graph-replayed SGHMC steps of config 2 (or another BASELINE config), fused update
+vs the separate update kernel, timed with events over K replayed steps; run under
+`rocprofv3 --kernel-trace --stats` for per-kernel durations."""
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "dgp-rf-mcmc_amd")]
+from dgprf import engine as E  # noqa: E402
+from dgprf.data import CONFIGS, classification_data, regression_data  # noqa: E402
+from likelihoods import Gaussian, Softmax  # noqa: E402
+from models.dgp import DGP_RF  # noqa: E402
+
+cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+modes = sys.argv[2].split(",") if len(sys.argv) > 2 else ["fused", "kernel"]
+steps = int(sys.argv[3]) if len(sys.argv) > 3 else 2000
+c = CONFIGS[cfg]
+dev = torch.device("cuda", 0)
+if c["likelihood"] == "softmax":
+    X, Y = classification_data(c["n"], c["d_in"], c["d_out"], seed=0, device=dev)
+    lik = Softmax()
+else:
+    X, Y, _ = regression_data(c["n"], c["d_in"], seed=0, device=dev)
+    lik = Gaussian(variance=c["variance"])
+for mode in modes:
+    E.Engine.fused_update = mode == "fused"
+    E.set_seed(3)
+    m = DGP_RF(c["d_in"], c["d_out"], n_hidden_layers=len(c["kinds"]), n_rf=c["n_rf"],
+               n_gp=c["n_gp"], likelihood=lik, kernel_type_list=c["kinds"])
+    m.precond_update(None, c["n"], precond_type="identity")
+    run = dict(batch_size=c["batch"], lr=c["lr"], momentum_decay=c["beta"], temperature=c["T"],
+               steps_per_graph=100)
+    m.run_sgmcmc(X, Y, c["n"], 200, **run)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    m.run_sgmcmc(X, Y, c["n"], steps, **run)
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / steps
+    print(f"config {cfg} {mode}: {us:.2f} us/step ({1e6 / us:.0f} steps/s) "
+          f"plan.fused_update={m._engine.plan_ws(c['batch'])[0].fused_update}", flush=True)

@@ -95,6 +95,31 @@ def pack(engine, per_layer):
 CASES = ["rbf2_gauss", "arc_rbf_softmax_cat", "mixed5", "wide_g"]
 
 
+@pytest.fixture(params=["kernel", "fused"])
+def update_path(request):
+    """Both W-only update paths: the per-step update kernel (default) and plan.fuse_update (the
+    update inside the step kernels; granted for these shapes)."""
+    from dgprf import engine as E
+    old = E.Engine.fused_update
+    E.Engine.fused_update = request.param == "fused"
+    yield request.param
+    E.Engine.fused_update = old
+
+
+@pytest.mark.parametrize("n,P,g", [(1000, 2048, 30), (77, 8192, 16), (5, 6, 1), (33, 130, 17)])
+def test_gp_layer_matmul(dev, n, P, g):
+    """Stand-alone GPLayer.__call__ (layers/GP_weight_layers.py:11-15) on the MFMA tile kernel:
+    ragged rows / outputs / K (P % 4 != 0 takes the scalar-load path) against float64 numpy."""
+    from layers import GPLayer
+    rng = np.random.default_rng(n + P)
+    gp = GPLayer(P, g)
+    W = rng.standard_normal((P, g)).astype(np.float32)
+    gp.assign_W(W)
+    X = (rng.standard_normal((n, P)) / np.sqrt(P)).astype(np.float32)
+    F = cpu(gp(X))
+    assert rel_err(F, X.astype(np.float64) @ W.astype(np.float64)) < 1e-5
+
+
 # ----------------------------------------------------------------------------- RNG
 def test_philox_normal_matches_oracle(dev):
     from dgprf import _native as N
@@ -167,7 +192,7 @@ def test_potential_grad(dev, golden, name):
 
 @pytest.mark.parametrize("name", CASES)
 @pytest.mark.parametrize("resample", [False, True])
-def test_sghmc_step_injected_noise(dev, golden, name, resample):
+def test_sghmc_step_injected_noise(dev, update_path, golden, name, resample):
     g = golden(name)
     m = model_from_fixture(g)
     eng = m._engine
@@ -187,7 +212,7 @@ def test_sghmc_step_injected_noise(dev, golden, name, resample):
         assert rel_err(cpu(eng.mom_view(l)), g[f"m1{sfx}_{l}"]) < 1e-4
 
 
-def test_config1_sgld_trajectory(dev, golden):
+def test_config1_sgld_trajectory(dev, update_path, golden):
     """Config 1 (1-layer RBF n_rf=100, mcycle-shaped N=133, full batch): 50 SGLD steps with
     injected noise track the float64 oracle trajectory."""
     from likelihoods import Gaussian
@@ -229,7 +254,7 @@ def test_standalone_update(dev, golden):
         assert rel_err(cpu(eng.mom_view(l)), m1) < 1e-5
 
 
-def test_device_philox_noise_counter(dev, golden):
+def test_device_philox_noise_counter(dev, update_path, golden):
     """The update's in-kernel noise is the Philox stream (seed, sub = step, NOISE, tag = chain)
     indexed by the packed element: a Philox step equals an injected-noise step."""
     g = golden("mixed5")
@@ -297,7 +322,7 @@ def test_epoch_minibatch_rows_bit_exact(dev):
         assert torch.equal(ge, gd), t
 
 
-def test_graph_replay_equals_eager_steps(dev):
+def test_graph_replay_equals_eager_steps(dev, update_path):
     from likelihoods import Gaussian
     from models.regression_model import RegressionDGP
     from dgprf import engine as E
@@ -317,11 +342,12 @@ def test_graph_replay_equals_eager_steps(dev):
     for _ in range(24):
         b._engine.step(X, Y, n, 0.01, 0.9, 1.0, batch_size=B, mode=2, perm_seed=3)
     assert int(a._engine.step_ctr) == 24 == int(b._engine.step_ctr)
+    assert a._engine.plan_ws(B)[0].fused_update == (update_path == "fused")
     assert torch.equal(a._engine.theta, b._engine.theta)
     assert torch.equal(a._engine.mom, b._engine.mom)
 
 
-def test_device_cyclical_schedule(dev):
+def test_device_cyclical_schedule(dev, update_path):
     """DGPRF_SCHED_CYCLICAL: burn-in lr0/T=0 then lr0 * rate^2, T=1 (utils_training.py:47-61)."""
     from likelihoods import Gaussian
     from models.regression_model import RegressionDGP
@@ -349,7 +375,7 @@ def test_device_cyclical_schedule(dev):
     assert rel_err(cpu(a._engine.theta), cpu(b._engine.theta)) < 1e-5
 
 
-def test_multichain_chain0_matches_single_chain(dev):
+def test_multichain_chain0_matches_single_chain(dev, update_path):
     from dgprf import engine as E
     from dgprf import _native as N
     spec = E.ModelSpec(3, 1, [N.RBF, N.ARC], [32, 48], [4, 1], False, N.LIK_GAUSSIAN)
