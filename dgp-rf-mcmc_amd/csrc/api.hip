@@ -118,6 +118,8 @@ hipError_t enqueue_step(const dgprf_plan_t& pl, const StepDev& sd, const UpdateD
                         bool pend0 = false, bool defer0 = false) {
   hipError_t e = hipSuccess;
   if (prep_gather) e = dgprf::launch_gather(pl, sd, s);
+  // random_fixed=False layers: this step's Omega from fresh z (layers/rf_layers.py:39-41)
+  if (e == hipSuccess && pl.fresh_z) e = dgprf::launch_fresh_omega(pl, sd, s);
   if (pl.fused_update && !sd.full_bayes && !ud.grad_only) {
     for (int l = 0; l < pl.n_layers && e == hipSuccess; ++l)
       e = dgprf::launch_step_fwd(pl, sd, l, s, &ud, l == 0 && pend0);
@@ -171,7 +173,8 @@ int dgprf_plan_init(dgprf_plan_t* pl) {
   if (pl->d_in < 1 || pl->d_out < 1 || pl->batch < 1 || pl->n_chains < 1) return DGPRF_E_SHAPE;
   if (pl->likelihood != DGPRF_LIK_GAUSSIAN && pl->likelihood != DGPRF_LIK_SOFTMAX) return DGPRF_E_ARG;
   if (pl->fwd_path < DGPRF_FWD_AUTO || pl->fwd_path > DGPRF_FWD_NO_AGEMM || pl->agemm_chunk_rows < 0 ||
-      (pl->fuse_update != 0 && pl->fuse_update != 1))
+      (pl->fuse_update != 0 && pl->fuse_update != 1) || pl->fresh_z < 0 ||
+      (pl->fresh_z >> L) != 0)
     return DGPRF_E_ARG;
   for (int l = 0; l < L; ++l) {
     if (pl->kind[l] != DGPRF_RBF && pl->kind[l] != DGPRF_ARC) return DGPRF_E_ARG;
@@ -261,6 +264,11 @@ int dgprf_plan_init(dgprf_plan_t* pl) {
   ws = align4(ws + (int64_t)B * pl->d_in);
   pl->yb_alt_off = ws;
   ws = align4(ws + (int64_t)B * pl->yb_cols);
+  pl->omf_off = -1;
+  if (pl->fresh_z) {
+    pl->omf_off = ws;
+    ws = align4(ws + om);
+  }
   pl->tick_off = ws;  // one 128-byte line per slice: tickets of different slices never share a
   ws = align4(ws + DGPRF_NS_MAX * 32);  // line (same-line atomics serialise at the memory side)
   // wide first layer: A_1 = X Omega_1 is one tiled GEMM per step (32-row tiles) instead of a
@@ -309,6 +317,7 @@ int dgprf_sghmc_step(const dgprf_plan_t* plan, const dgprf_chain_t* chain,
   if (!rc) rc = check_step(step);
   if (rc) return rc;
   if (step->full_bayes && (rc = check_full_bayes(*plan, *chain))) return rc;
+  if (step->full_bayes && plan->fresh_z) return DGPRF_E_ARG;
   dgprf_step_t st = *step;
   st.grad_only = 0;
   StepDev sd = make_step_dev(*plan, *chain, *batch, st.step_offset);
@@ -328,6 +337,7 @@ int dgprf_potential_grad(const dgprf_plan_t* plan, const dgprf_chain_t* chain,
   if (rc) return rc;
   if (!grad_out || !(data_size > 0.f)) return DGPRF_E_ARG;
   if (full_bayes && (rc = check_full_bayes(*plan, *chain))) return rc;
+  if (full_bayes && plan->fresh_z) return DGPRF_E_ARG;
   StepDev sd = make_step_dev(*plan, *chain, *batch, 0);
   sd.grad_out = grad_out;
   sd.full_bayes = full_bayes != 0;
@@ -352,6 +362,7 @@ int dgprf_graph_create_sghmc(dgprf_graph_handle* out, const dgprf_plan_t* plan,
       step->xi_hyp_resample)
     return DGPRF_E_ARG;
   if (step->full_bayes && (rc = check_full_bayes(*plan, *chain))) return rc;
+  if (step->full_bayes && plan->fresh_z) return DGPRF_E_ARG;
   hipStream_t cs;
   if (hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess) return DGPRF_E_HIP;
   hipError_t e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);

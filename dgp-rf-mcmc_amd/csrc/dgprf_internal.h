@@ -111,6 +111,9 @@ hipError_t launch_gather(const dgprf_plan_t& pl, const StepDev& sd, hipStream_t 
 hipError_t launch_agemm(const float* X, int64_t n, int ld, int d, const float* om, int R,
                         float* aout, hipStream_t s);
 hipError_t launch_advance(int64_t* step, int64_t by, hipStream_t s);
+// plan.fresh_z: Omega of every layer into the workspace (omf_off), fresh layers from Philox z of
+// step *step + step_offset, the others copied from the chain's Omega
+hipError_t launch_fresh_omega(const dgprf_plan_t& pl, const StepDev& sd, hipStream_t s);
 
 // How dgprf_forward covers n rows: tile or row kernel, the A_1 GEMM for a wide first layer (in
 // row chunks of `chunk` rows of caller scratch).  Host-only, shared by the launcher and the

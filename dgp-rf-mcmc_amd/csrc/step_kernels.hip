@@ -81,6 +81,10 @@ struct LayerK {
   int32_t pend;         // forward, layer 0: apply the previous step's pending W_1 update first
   int32_t pend_lo;      // w_off of layer 0
   int32_t smap, pad_s;  // slice-major block map (tile_of_block)
+  // whole-slice staging (backward, cpw >= 4): the workgroup's W rows [h][64 cpw][g] and Omega rows
+  // [dxw][64 cpw + 4] are copied global -> LDS once (global_load_lds) instead of one 64-feature
+  // block per chunk with a load round trip and two barriers each
+  int32_t wstage, wsa_off, osa_off, osa_st, kind_rbf, pad_w;
   int32_t main_blocks;  // this layer's (row tile, slice) workgroups; extra workgroups follow
   int32_t upd_blocks, upd_layer, upd_lo, upd_hi;  // backward extras: the update of layer upd_layer's
                                                   // W (packed range [upd_lo, upd_hi))
@@ -761,6 +765,34 @@ __global__ __launch_bounds__(256) void k_step_fwd(const LayerK a) {
 }
 
 // ------------------------------------------------------------------------- backward
+// Whole-slice staging (a.wstage): W rows [fb0, fb0 + 64 cpw) of both halves (contiguous runs of
+// 64 cpw g floats in W) and Omega rows k < dxw over the same features (runs of 64 cpw floats, one
+// LDS row of 64 cpw + 4 each) as 16-byte global_load_lds: lane-linear LDS destinations, no VGPRs,
+// every copy in flight at once; the prologue's barrier waits for them.  The slice lies inside the
+// layer (R % (64 cpw) == 0) and every run starts 16-byte aligned (R g % 4 == 0).
+__device__ __forceinline__ void stage_slice_lds(const LayerK& a, const float* W, const float* om,
+                                                int fb0, float* smem) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nf = 64 * a.cpw, g = a.g, R = a.R;
+  const int n4 = nf * g / 4;  // float4 per half
+  const int nh = a.kind_rbf ? 2 : 1;
+  for (int h = 0; h < nh; ++h) {
+    const float* src = W + ((int64_t)h * R + fb0) * g;
+    float* dst = smem + a.wsa_off + h * nf * g;
+    for (int i0 = wave * 64; i0 < n4; i0 += 256) {
+      if (i0 + lane < n4)
+        __builtin_amdgcn_global_load_lds(src + 4 * (i0 + lane), dst + 4 * i0, 16, 0, 0);
+    }
+  }
+  const int per_row = nf / 256;  // 256-float instructions per Omega row (cpw >= 4)
+  for (int j = wave; j < a.dxw * per_row; j += 4) {
+    const int k = j / per_row, c = j - k * per_row;
+    __builtin_amdgcn_global_load_lds(om + (int64_t)k * R + fb0 + c * 256 + 4 * lane,
+                                     smem + a.osa_off + k * a.osa_st + c * 256, 16, 0, 0);
+  }
+}
+
+
 template <int KS, int NOT, bool RBF, bool G1, bool FB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NOT == 1 && !FB && (KS == 1 || KS == 2 || (KS == 4 && !RBF))) ? DGPRF_STEP_WPE : 1))) void k_step_bwd(const LayerK a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -850,7 +882,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NOT == 1 &
   if (a.fast) {
     // ---- single burst: W/Omega block, X tile, dF (or F_L) partials and Y rows
     f4 sw[2], so;
-    if (dphi) {
+    if (dphi && a.wstage) stage_slice_lds(a, W, om, fb0, smem);
+    if (dphi && !a.wstage) {
       const rsrc_t rw = make_rsrc(W, (int64_t)(RBF ? 2 : 1) * R * g);
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
@@ -864,14 +897,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NOT == 1 &
     }
     DGPRF_STAMP(stamp_base, 1);
     elem_prologue(a, chain, row0, TR * g, xs, dfs, dfst, ysh, red);
-    if (dphi) {
+    if (dphi && !a.wstage) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) *reinterpret_cast<f4*>(wsl + 4 * ((int)threadIdx.x + 256 * j)) = sw[j];
       *reinterpret_cast<f4*>(osl + (threadIdx.x >> 4) * OST + 4 * (threadIdx.x & 15)) = so;
     }
     DGPRF_STAMP(stamp_base, 4);
   } else {
-    if (dphi) stage_load(fb0);
+    if (dphi && a.wstage) stage_slice_lds(a, W, om, fb0, smem);
+    if (dphi && !a.wstage) stage_load(fb0);
     if (KS > 0 || !a.a0 || FB) load_x_tile(a, chain, row0, xs);
     for (int e = threadIdx.x; e < TR * g; e += blockDim.x) {  // dF (or F_L) slice sums; Y alongside
       const int r = e / g, o = e - r * g, b = row0 + r, bc = min(b, B - 1);
@@ -930,7 +964,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NOT == 1 &
       }
     }
   }
-  if (!a.fast && dphi) stage_store(fb0);
+  if (!a.fast && dphi && !a.wstage) stage_store(fb0);
   __syncthreads();
   DGPRF_STAMP(stamp_base, 2);
 
@@ -979,7 +1013,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NOT == 1 &
       if (FB)
 #pragma unroll
         for (int dt = 0; dt < NZ; ++dt) zpf[dt] = z_frag(f0, dt);
-      if (dphi) {
+      if (dphi && !a.wstage) {
         stage_load((sl * cpw + i) * 64);
         __syncthreads();  // every wave is done with the previous block
         stage_store((sl * cpw + i) * 64);
@@ -992,19 +1026,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NOT == 1 &
     //   dPhi = dF W^T in the features-in-registers orientation (K = g)
     float wd0[KGM], wd1[KGM];
     f4 oxv[4];
+    // this chunk's 64-feature block: the per-chunk staging buffers, or its rows of the slice image
+    const float* wsc = a.wstage ? smem + a.wsa_off + i * 64 * g : wsl;
+    const int whalf = a.wstage ? 64 * cpw * g : nwh;
+    const float* osc = a.wstage ? smem + a.osa_off + i * 64 : osl;
+    const int ostc = a.wstage ? a.osa_st : OST;
     if (dphi) {
       const bool frow = f0 + lr < R;
 #pragma unroll
       for (int ks = 0; ks < KGM; ++ks) {
         const int o = 4 * ks + lq, wo = (wave * 16 + lr) * g + o;
         const bool ok = o < g && frow;
-        wd0[ks] = G1 ? 0.f : (ok ? wsl[wo] : 0.f);
-        wd1[ks] = (G1 || !RBF) ? 0.f : (ok ? wsl[nwh + wo] : 0.f);
+        wd0[ks] = G1 ? 0.f : (ok ? wsc[wo] : 0.f);
+        wd1[ks] = (G1 || !RBF) ? 0.f : (ok ? wsc[whalf + wo] : 0.f);
       }
       // rows k >= dxw of the staged block are never written: they only feed discarded outputs
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt)
-        oxv[dt] = *reinterpret_cast<const f4*>(osl + (dt * 16 + lr) * OST + wave * 16 + 4 * lq);
+        oxv[dt] = *reinterpret_cast<const f4*>(osc + (dt * 16 + lr) * ostc + wave * 16 + 4 * lq);
     }
     // layer 0 with d > 32: both orientations read the precomputed A_1 (k_step_agemm)
     const float* a0 = KS == 0 && a.a0 ? a.a0 + (int64_t)chain * a.ws_cs + (int64_t)row0 * R + f0
@@ -1026,8 +1065,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NOT == 1 &
         for (int r = 0; r < 4; ++r) {
           const int fl = wave * 16 + 4 * lq + r;
           const bool ok = f0 + 4 * lq + r < R;
-          dpc[r] = ok ? dg1 * wsl[fl] : 0.f;
-          dps[r] = (ok && RBF) ? dg1 * wsl[64 + fl] : 0.f;
+          dpc[r] = ok ? dg1 * wsc[fl] : 0.f;
+          dps[r] = (ok && RBF) ? dg1 * wsc[whalf + fl] : 0.f;
         }
       } else {
 #pragma unroll
@@ -1604,6 +1643,36 @@ __global__ __launch_bounds__(UPD_THREADS) void k_step_update(const UpdK a) {
 }
 
 
+// random_fixed=False (layers/rf_layers.py:39-41): Omega_l = exp(lis_l)[:,None] z + mean_l[:,None]
+// with z ~ N(0,1) drawn for this step — Philox (seed, sub = step, DGPRF_RNG_Z, tag = 1 + l + 16
+// chain), element i of the layer at counter quad i / 4 — for the fresh layers.  One thread per
+// 4 elements; chain blockIdx.y writes its own workspace copy.
+__global__ void k_fresh_omega(const dgprf_plan_t pl, const float* __restrict__ hyp, float* ws,
+                              const int64_t* step, uint64_t seed, int32_t step_offset) {
+  const int chain = blockIdx.y;
+  const int64_t i0 = 4 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+  if (i0 >= pl.omega_total) return;
+  int layer = 0;
+  for (int l = 1; l < pl.n_layers; ++l)
+    if (i0 >= pl.omega_off[l]) layer = l;
+  if (!((pl.fresh_z >> layer) & 1)) return;
+  const float* h = hyp + (pl.hyp_per_chain ? (int64_t)chain * pl.hyp_total : 0);
+  float* om = ws + (int64_t)chain * pl.ws_chain + pl.omf_off;
+  const int64_t n_l = (int64_t)pl.d[layer] * pl.n_rf[layer];
+  const int64_t j0 = i0 - pl.omega_off[layer];  // omega_off is a multiple of 4
+  const int64_t t = *step + step_offset;
+  const f4 z = philox_normal4(seed, (uint64_t)t, DGPRF_RNG_Z, 1u + layer + 16u * chain,
+                              (uint32_t)(j0 >> 2));
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int64_t j = j0 + c;
+    if (j < n_l) {
+      const int k = (int)(j / pl.n_rf[layer]);
+      om[pl.omega_off[layer] + j] = expf(h[pl.lis_off[layer] + k]) * z[c] + h[pl.mean_off[layer] + k];
+    }
+  }
+}
+
 __global__ void k_advance(int64_t* step, int64_t by) {
   if (threadIdx.x == 0 && blockIdx.x == 0) *step += by;
 }
@@ -1693,10 +1762,13 @@ __global__ __launch_bounds__(256) void k_step_agemm(const AgemmK a) {
   }
 }
 
-LayerK make_layer_k(const dgprf_plan_t& pl, const StepDev& sd, int l, int& lds_floats) {
+LayerK make_layer_k(const dgprf_plan_t& pl, const StepDev& sd, int l, int& lds_floats,
+                    bool bwd = false) {
   LayerK a;
   const bool direct = sd.bd.mode == DGPRF_BATCH_DIRECT;
-  a.om = sd.omega + pl.omega_off[l];
+  // random_fixed=False layers read this step's Omega from the workspace (k_fresh_omega)
+  const bool fresh = ((pl.fresh_z >> l) & 1) && pl.omf_off >= 0;
+  a.om = fresh ? sd.ws + pl.omf_off + pl.omega_off[l] : sd.omega + pl.omega_off[l];
   a.W = sd.theta + pl.w_off[l];
   a.fprev = l > 0 ? sd.ws + pl.fp_off[l - 1] : sd.ws;
   a.fout = sd.ws + pl.fp_off[l];
@@ -1711,7 +1783,7 @@ LayerK make_layer_k(const dgprf_plan_t& pl, const StepDev& sd, int l, int& lds_f
   a.y_cols = direct ? sd.bd.y_cols : pl.yb_cols;
   a.cptr = sd.der + l;
   a.varptr = sd.der + DGPRF_MAX_LAYERS;
-  a.om_cs = sd.om_cs;
+  a.om_cs = fresh ? pl.ws_chain : sd.om_cs;
   a.der_cs = sd.der_cs;
   a.w_cs = pl.w_total;
   a.ws_cs = pl.ws_chain;
@@ -1745,6 +1817,24 @@ LayerK make_layer_k(const dgprf_plan_t& pl, const StepDev& sd, int l, int& lds_f
   a.hp = sd.ws + pl.hpp_off[l];
   a.hpl = sd.ws + pl.hpl_off;
   a.lik_fb = (pl.hyp_flags & DGPRF_HYP_LIK) != 0 && pl.likelihood == DGPRF_LIK_GAUSSIAN;
+  // whole-slice staging for the backward (used only where dPhi / dX need W and Omega)
+  a.kind_rbf = pl.kind[l] == DGPRF_RBF;
+  a.pad_w = 0;
+  a.wstage = 0;
+  a.wsa_off = a.osa_off = a.osa_st = 0;
+  {
+    const int nf = 64 * a.cpw, nh = a.kind_rbf ? 2 : 1;
+    const int wsa = a.stg_off, osa = wsa + round4(nh * nf * a.g), ost = nf + 4;
+    const int end = osa + a.dxw * ost + (sd.full_bayes ? NW * round4(2 * a.d + 1) : 0);
+    if (bwd && a.cpw % 4 == 0 && a.R % nf == 0 && ((int64_t)a.R * a.g) % 4 == 0 &&
+        end <= 38 * 1024) {
+      a.wstage = 1;
+      a.wsa_off = wsa;
+      a.osa_off = osa;
+      a.osa_st = ost;
+      lds_floats = max(lds_floats, osa + a.dxw * ost);
+    }
+  }
   a.hred_off = lds_floats;
   if (sd.full_bayes) lds_floats += NW * round4(2 * a.d + 1);
   // fused update: off unless the launcher sets it up (fill_fused)
@@ -1945,7 +2035,7 @@ hipError_t launch_step_fwd(const dgprf_plan_t& pl, const StepDev& sd, int layer,
 hipError_t launch_step_bwd(const dgprf_plan_t& pl, const StepDev& sd, int layer, hipStream_t s,
                            const UpdateDev* ud, bool gather_next) {
   int lds_floats = 0;
-  LayerK a = make_layer_k(pl, sd, layer, lds_floats);
+  LayerK a = make_layer_k(pl, sd, layer, lds_floats, /*bwd=*/true);
   if (ud && pl.fused_update) {
     fill_fused(a, pl, sd, *ud);
     // extra workgroups: W_{l+2}'s update from the gW partials layer l+1's backward just wrote
@@ -2120,6 +2210,15 @@ hipError_t launch_gather(const dgprf_plan_t& pl, const StepDev& sd, hipStream_t 
   const int rows_per_block = pl.d_in > GATHER_WIDE ? 4 : 256;
   dim3 grid((unsigned)((pl.batch + rows_per_block - 1) / rows_per_block), pl.n_chains);
   hipLaunchKernelGGL(k_gather, grid, dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_fresh_omega(const dgprf_plan_t& pl, const StepDev& sd, hipStream_t s) {
+  if (!sd.hyp) return hipErrorInvalidValue;
+  const int64_t quads = (pl.omega_total + 3) / 4;
+  dim3 grid((unsigned)((quads + 255) / 256), pl.n_chains);
+  hipLaunchKernelGGL(k_fresh_omega, grid, dim3(256), 0, s, pl, sd.hyp, sd.ws, sd.step, sd.seed,
+                     sd.step_offset);
   return hipGetLastError();
 }
 

@@ -42,7 +42,7 @@ class Plan(ctypes.Structure):
         ("likelihood", _i32), ("batch", _i32), ("n_chains", _i32),
         ("kind", _i32 * _L), ("n_rf", _i32 * _L), ("n_gp", _i32 * _L),
         ("hyp_flags", _i32), ("hyp_per_chain", _i32), ("ard", _i32 * _L),
-        ("fwd_path", _i32), ("agemm_chunk_rows", _i32), ("fuse_update", _i32), ("pad_c", _i32),
+        ("fwd_path", _i32), ("agemm_chunk_rows", _i32), ("fuse_update", _i32), ("fresh_z", _i32),
         ("initialised", _i32),
         ("d", _i32 * _L), ("P", _i32 * _L), ("ns", _i32 * _L), ("cpw", _i32 * _L),
         ("n_row_tiles", _i32), ("n_rt_pad", _i32),
@@ -53,7 +53,7 @@ class Plan(ctypes.Structure):
         ("ws_chain", _i64), ("ws_total", _i64), ("hpp_off", _i64 * _L), ("hpl_off", _i64),
         ("xb_off", _i64), ("yb_off", _i64),
         ("yb_cols", _i32), ("fused_update", _i32), ("a0_off", _i64),
-        ("xb_alt_off", _i64), ("yb_alt_off", _i64), ("tick_off", _i64),
+        ("xb_alt_off", _i64), ("yb_alt_off", _i64), ("omf_off", _i64), ("tick_off", _i64),
     ]
 
 

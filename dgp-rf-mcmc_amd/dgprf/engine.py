@@ -226,16 +226,19 @@ class Engine:
         return self.hyp[c * pl.hyp_total:(c + 1) * pl.hyp_total]
 
     # ---------------------------------------------------------------- per-B plans
-    def plan_ws(self, B):
-        B = int(B)
-        if B not in self._ws:
-            pl = self.spec.plan(B, self.C, self.per_chain_hyp)
-            if self.fused_update:  # request the fused W-only update (plan_init grants or not)
-                pl.fuse_update = 1
+    def plan_ws(self, B, fresh_z=0):
+        """(plan, zero-filled workspace) for minibatch size B; fresh_z = bit mask of the layers
+        that draw fresh z every step on the device (random_fixed=False, graph steps)."""
+        key = (int(B), int(fresh_z))
+        if key not in self._ws:
+            pl = self.spec.plan(key[0], self.C, self.per_chain_hyp)
+            if self.fused_update or fresh_z:
+                pl.fuse_update = int(bool(self.fused_update))  # request (plan_init grants or not)
+                pl.fresh_z = key[1]
                 N.call("dgprf_plan_init", ctypes.byref(pl))
             ws = torch.zeros(max(pl.ws_total, 4), dtype=_F32, device=self.dev)
-            self._ws[B] = (pl, ws)
-        return self._ws[B]
+            self._ws[key] = (pl, ws)
+        return self._ws[key]
 
     def chain_struct(self, ws, omega=None, z=None):
         c = N.Chain()
@@ -379,21 +382,22 @@ class Engine:
 
     def graph(self, X_all, Y_all, batch_size, data_size, lr, beta, T, steps_per_graph,
               schedule=N.SCHED_CONST, start_step=0, cycle_length=1, resample_head=False,
-              perm_seed=0, full_bayes=False):
-        """hipGraph of `steps_per_graph` on-device-minibatched steps (DGPRF_BATCH_EPOCH)."""
+              perm_seed=0, full_bayes=False, fresh_z=0):
+        """hipGraph of `steps_per_graph` on-device-minibatched steps (DGPRF_BATCH_EPOCH);
+        fresh_z: layers (bit mask) whose z is redrawn every step (random_fixed=False)."""
         if full_bayes:
             self._check_full_bayes()
         key = (X_all.data_ptr(), tuple(X_all.shape), Y_all.data_ptr(), tuple(Y_all.shape),
                int(batch_size), float(data_size), float(lr), float(beta), float(T),
                int(steps_per_graph), int(schedule), int(start_step), int(cycle_length),
-               bool(resample_head), int(perm_seed), bool(full_bayes))
+               bool(resample_head), int(perm_seed), bool(full_bayes), int(fresh_z))
         if key in self._graphs:
             g = self._graphs.pop(key)  # most recently used last
             self._graphs[key] = g
             return g
         while len(self._graphs) >= self.MAX_GRAPHS:  # bounded: evict the least recently used
             self._graphs.pop(next(iter(self._graphs)))
-        pl, ws = self.plan_ws(batch_size)
+        pl, ws = self.plan_ws(batch_size, fresh_z)
         iters = X_all.shape[0] // int(batch_size)
         ch = self.chain_struct(ws)
         bt = self.batch_struct(X_all, Y_all, N.BATCH_EPOCH, iters=iters, perm_seed=perm_seed)

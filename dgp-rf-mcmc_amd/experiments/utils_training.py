@@ -12,8 +12,9 @@ the end of each cycle.  Here a whole epoch of steps is ONE hipGraph replay: mini
 on the device (per-epoch permutation, drop remainder), and the burn-in / cosine schedule and the
 cycle-head momentum resampling are evaluated inside the update kernel from the device step counter
 (DGPRF_SCHED_CYCLICAL, the same float32 formula as utils.py:49-73 with min_value = 0).  The host
-only launches graphs and scores samples.  Models with random_fixed=False (fresh z per call) or
-datasets that are not DeviceDatasets take the reference's per-batch loop instead.
+only launches graphs and scores samples.  random_fixed=False layers redraw z every step on the
+device (Philox keyed on the step counter).  Full-Bayes sampling of such a model, and datasets that
+are not DeviceDatasets, take the reference's per-batch loop instead.
 
 Deliberate differences: samples are COPIES of W (the reference appends the
 live variables, so every stored "sample" aliases the current W; set REFERENCE_SAMPLE_ALIASING = True
@@ -35,10 +36,11 @@ def _store_W(model):
     return [W.detach().clone() for W in model.W_mcmc]
 
 
-def _graph_ok(model, ds_train):
+def _graph_ok(model, ds_train, full_bayesian=False):
     return (isinstance(ds_train, DeviceDataset) and ds_train.drop_remainder and
             ds_train.batch_size is not None and
-            all(model.BNN.layers[2 * l].random_fixed for l in range(model.n_hidden_layers)))
+            (not full_bayesian or
+             all(model.BNN.layers[2 * l].random_fixed for l in range(model.n_hidden_layers))))
 
 
 def _run_epochs(model, ds_train, ds_M, data_size, batch_size, lr_0, momentum_decay,
@@ -49,7 +51,7 @@ def _run_epochs(model, ds_train, ds_M, data_size, batch_size, lr_0, momentum_dec
     iterations_per_epoch = ds_train.num_batches() if isinstance(ds_train, DeviceDataset) \
         else sum(1 for _ in ds_train)
     cycle_length = epochs_per_cycle * iterations_per_epoch
-    graph = _graph_ok(model, ds_train)
+    graph = _graph_ok(model, ds_train, full_bayesian)
     if graph:
         # schedule clock: the device step counter at the driver's first step is step_index 1 of
         # the burn-in; sampling starts start_sampling_epoch epochs later

@@ -426,8 +426,12 @@ class DGP_RF(Module):
         are returned."""
         self._check_moments(full_bayesian)
         eng = self._engine
-        if not all(self.BNN.layers[2 * l].random_fixed for l in range(self.n_hidden_layers)):
-            raise NotImplementedError("run_sgmcmc needs random_fixed=True")
+        # random_fixed=False layers redraw z on every call (layers/rf_layers.py:39-41): on the
+        # device, from the step's Philox counter, inside the graph
+        fresh = sum(1 << l for l in range(self.n_hidden_layers)
+                    if not self.BNN.layers[2 * l].random_fixed)
+        if fresh and full_bayesian:
+            raise NotImplementedError("run_sgmcmc with random_fixed=False needs full_bayesian=False")
         X_all = E.as_device(X_all, eng.dev)
         Y_all = E.as_device(Y_all, eng.dev)
         if Y_all.dim() == 1:
@@ -436,7 +440,8 @@ class DGP_RF(Module):
         spg = max(1, min(int(steps_per_graph), int(n_steps)))
         mk = lambda k: eng.graph(X_all, Y_all, batch_size, data_size, lr, momentum_decay,
                                  temperature, k, sched, start_step, cycle_length,
-                                 resample_in_cycle_head, perm_seed, full_bayes=bool(full_bayesian))
+                                 resample_in_cycle_head, perm_seed, full_bayes=bool(full_bayesian),
+                                 fresh_z=fresh)
         eng.build_omega()
         full, rest = divmod(int(n_steps), spg)
         plan = [(mk(spg), full)] if full else []

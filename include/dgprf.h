@@ -120,7 +120,10 @@ typedef struct dgprf_plan {
   int32_t agemm_chunk_rows; /* wide first layer: rows of A_1 per dgprf_forward chunk (0 = as many as
                                fit 64M floats; otherwise rounded down to a multiple of 64, >= 64) */
   int32_t fuse_update;     /* 1: request the fused W-only update (see fused_update below) */
-  int32_t pad_c;
+  int32_t fresh_z;         /* bit l: layer l draws fresh z ~ N(0,1) every step (random_fixed=False,
+                              layers/rf_layers.py:39-41): the step builds that layer's Omega from
+                              Philox (seed, sub = step, DGPRF_RNG_Z, tag = 1 + l + 16 chain) into
+                              the workspace (omf_off).  W-only steps (not full_bayes). */
   /* ---- derived by dgprf_plan_init ---- */
   int32_t initialised;
   int32_t d[DGPRF_MAX_LAYERS];      /* layer input width */
@@ -161,6 +164,8 @@ typedef struct dgprf_plan {
                                         MFMA GEMM per step (per chain); -1 when not used          */
   int64_t xb_alt_off;                /* second gathered-rows buffers (graph steps alternate      */
   int64_t yb_alt_off;                /*   between the two by step parity)                       */
+  int64_t omf_off;                   /* fresh_z != 0: this step's Omega of every layer [omega_total]
+                                        (per chain; fresh layers rebuilt each step); -1 otherwise */
   int64_t tick_off;                  /* [16][32] uint32 arrival tickets of the deferred W_1
                                         update, one 128-byte line per feature slice (per chain;
                                         zero between launches)                                   */

@@ -347,6 +347,41 @@ def test_graph_replay_equals_eager_steps(dev, update_path):
     assert torch.equal(a._engine.mom, b._engine.mom)
 
 
+def test_graph_fresh_z_random_fixed_false(dev, update_path):
+    """random_fixed=False inside graph-replayed steps (layers/rf_layers.py:39-41): every step draws
+    z ~ N(0,1) on the device from Philox (seed, sub = step, RNG_Z, tag = 1 + layer) and builds that
+    step's Omega; 3 graph steps equal 3 eager steps of a random_fixed=True twin whose z is set to
+    the same draws (oracle Philox) before each step."""
+    from dgprf import engine as E
+    from likelihoods import Gaussian
+    from models.regression_model import RegressionDGP
+    E.set_seed(21)
+    a = RegressionDGP(3, 1, n_hidden_layers=2, n_rf=[32, 24], n_gp=[4, 1],
+                      likelihood=Gaussian(variance=0.2), random_fixed=False)
+    b = RegressionDGP(3, 1, n_hidden_layers=2, n_rf=[32, 24], n_gp=[4, 1],
+                      likelihood=Gaussian(variance=0.2))
+    n, B = 320, 32
+    X = torch.randn(n, 3, device=dev)
+    Y = torch.randn(n, 1, device=dev)
+    for mm in (a, b):
+        mm.precond_update(None, n, precond_type="identity")
+    ea, eb = a._engine, b._engine
+    for t in ("theta", "mom", "hyp", "step_ctr"):
+        getattr(eb, t).copy_(getattr(ea, t))
+    eb.seed = ea.seed
+    a.run_sgmcmc(X, Y, n, 3, batch_size=B, lr=0.01, momentum_decay=0.9, steps_per_graph=3,
+                 perm_seed=5)
+    pl = eb.layout
+    for t in range(3):
+        for l in range(2):
+            nz = pl.d[l] * pl.n_rf[l]
+            z = R.philox_normal(nz, eb.seed, t, R.PURPOSE_Z, tag=1 + l)
+            eb.z_view(l).copy_(torch.as_tensor(z.reshape(pl.d[l], pl.n_rf[l]), dtype=torch.float32))
+        eb.step(X, Y, n, 0.01, 0.9, 1.0, batch_size=B, mode=2, perm_seed=5)
+    assert int(ea.step_ctr) == 3 == int(eb.step_ctr)
+    assert rel_err(cpu(ea.theta), cpu(eb.theta)) < 1e-5
+
+
 def test_device_cyclical_schedule(dev, update_path):
     """DGPRF_SCHED_CYCLICAL: burn-in lr0/T=0 then lr0 * rate^2, T=1 (utils_training.py:47-61)."""
     from likelihoods import Gaussian
