@@ -120,6 +120,7 @@ hipError_t launch_fresh_omega(const dgprf_plan_t& pl, const StepDev& sd, hipStre
 // scratch query so both size the chunks identically.
 struct ForwardCfg {
   bool wide0, tiles;
+  int rows_waves;  // waves per 16-row tile of the row kernel (4 or 16)
   int64_t chunk, scratch_floats;
 };
 ForwardCfg forward_cfg(const dgprf_plan_t& pl, int64_t n);

@@ -28,7 +28,7 @@ struct FwdLds {
   int xst, ftst, red_off, ft_off, total;
 };
 
-__host__ __device__ inline FwdLds fwd_lds(const dgprf_plan_t& pl) {
+__host__ __device__ inline FwdLds fwd_lds(const dgprf_plan_t& pl, int nwr = NW) {
   int dmax = 4, gmax = 1;
   for (int l = 0; l < pl.n_layers; ++l) {
     dmax = pl.d[l] > dmax ? pl.d[l] : dmax;
@@ -38,7 +38,7 @@ __host__ __device__ inline FwdLds fwd_lds(const dgprf_plan_t& pl) {
   L.xst = round4(dmax) + 1;
   L.ftst = round4(gmax) + 1;
   L.red_off = round4(TR * L.xst);
-  L.ft_off = L.red_off + NW * TR * 64;
+  L.ft_off = L.red_off + nwr * TR * 64;
   L.total = L.ft_off + round4(TR * L.ftst);
   return L;
 }
@@ -47,28 +47,35 @@ struct FOut {
   float* p[DGPRF_MAX_LAYERS];
 };
 
-// One wave's F partial of one layer over its features (chunks wave, wave+4, ...), written to
-// red[wave][16][NOT*16].  Fragments of the next chunk are loaded before the current chunk's MFMAs;
-// cos and sin products accumulate in separate chains.  G1 (g == 1): the W^T Phi^T product is a
-// per-lane dot product (VALU) reduced over the 4 lane groups, instead of a 16x16 MFMA tile that
-// would be 15/16 padding.
-template <bool SMALLD, int NOT, bool RBF, bool G1>
+// One wave's F partial of one layer over its features (chunks wave, wave + NWR, ...), written to
+// red[wave][16][NOT*16].  Chunks go in groups of CG (4 for 4-wave tiles with NOT == 1, else 2): the group's Omega / W
+// fragments are loaded together (one L2 round trip per group instead of per chunk) and its chunks'
+// MFMA chains are independent; cos and sin products accumulate in separate chains.  G1 (g == 1):
+// the W^T Phi^T product is a per-lane dot product (VALU) reduced over the 4 lane groups, instead of
+// a 16x16 MFMA tile that would be 15/16 padding.
+template <bool SMALLD, int NOT, bool RBF, bool G1, int NWR>
 __device__ __forceinline__ void layer_partial(const float* __restrict__ om,
                                               const float* __restrict__ W, int R, int d, int g,
                                               float cl, const float* xs, int xst, float* red,
                                               int wave, int lr, int lq,
                                               const float* __restrict__ arow = nullptr) {
+  constexpr int CG = (NWR >= 16 || NOT > 1) ? 2 : 4;
   float xf[8];
 #pragma unroll
   for (int ks = 0; ks < 8; ++ks) xf[ks] = (SMALLD && 4 * ks < d) ? xs[lr * xst + 4 * ks + lq] : 0.f;
-  float omk[8], wf[NOT][4][2];
-  auto load_frag = [&](int f0) {
+  const int nks = (d + 3) >> 2;  // k-steps (SMALLD: <= 8)
+  float omk[CG][8], wf[CG][NOT][4][2];
+  // buffer loads: 32-bit offsets (one VGPR per address), masked lanes read 0 without traffic
+  const rsrc_t ro = make_rsrc(om, SMALLD ? (int64_t)d * R : 0);
+  const rsrc_t rw = make_rsrc(W, (int64_t)(RBF ? 2 : 1) * R * g);
+  auto load_frag = [&](int j, int f0) {
     const int fa = f0 + lr;
     if (SMALLD) {
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks) {
         const int k = 4 * ks + lq;
-        omk[ks] = (4 * ks < d && fa < R && k < d) ? om[(int64_t)k * R + fa] : 0.f;
+        omk[j][ks] = ks < nks ? bload1(ro, fa < R && k < d ? (uint32_t)((k * R + fa) * 4) : DGPRF_OOB)
+                              : 0.f;
       }
     }
 #pragma unroll
@@ -78,8 +85,8 @@ __device__ __forceinline__ void layer_partial(const float* __restrict__ om,
       for (int r = 0; r < 4; ++r) {
         const int fr = f0 + 4 * lq + r;
         const bool ok = o < g && fr < R;
-        wf[ot][r][0] = ok ? W[(int64_t)fr * g + o] : 0.f;
-        wf[ot][r][1] = (RBF && ok) ? W[(int64_t)(R + fr) * g + o] : 0.f;
+        wf[j][ot][r][0] = bload1(rw, ok ? (uint32_t)((fr * g + o) * 4) : DGPRF_OOB);
+        wf[j][ot][r][1] = RBF ? bload1(rw, ok ? (uint32_t)(((R + fr) * g + o) * 4) : DGPRF_OOB) : 0.f;
       }
     }
   };
@@ -87,61 +94,58 @@ __device__ __forceinline__ void layer_partial(const float* __restrict__ om,
 #pragma unroll
   for (int ot = 0; ot < NOT; ++ot) acc[ot] = acs[ot] = f4zero();
   float dot = 0.f;
-  int f0 = wave * 16;
-  if (f0 < R) load_frag(f0);
-  for (; f0 < R; f0 += NW * 16) {
-    f4 at = f4zero();
-    if (SMALLD) {
+  constexpr int STEP = NWR * 16;
+  for (int base = wave * 16; base < R; base += CG * STEP) {
 #pragma unroll
-      for (int ks = 0; ks < 8; ++ks)
-        if (4 * ks < d) at = mfma16(omk[ks], xf[ks], at);
-    } else if (arow) {  // precomputed A row (wide first layer): A[row lr][f0 + 4lq + r]
-      at = *reinterpret_cast<const f4*>(arow + f0 + 4 * lq);
-    } else {
-      const int fa = f0 + lr;
-      const int KS = round4(d) >> 2;
-      for (int ks = 0; ks < KS; ++ks) {
-        const int k = 4 * ks + lq;
-        const float o = (fa < R && k < d) ? om[(int64_t)k * R + fa] : 0.f;
-        at = mfma16(o, xs[lr * xst + 4 * ks + lq], at);
-      }
-    }
-    float p0[4], p1[4];
+    for (int j = 0; j < CG; ++j)
+      if (base + j * STEP < R) load_frag(j, base + j * STEP);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      if (RBF) {
-        float s, c;
-        rf_sincos(at[r], &s, &c);
-        p0[r] = cl * c;
-        p1[r] = cl * s;
+    for (int j = 0; j < CG; ++j) {
+      const int f0 = base + j * STEP;
+      if (f0 >= R) break;
+      f4 at = f4zero();
+      if (SMALLD) {
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks)
+          if (ks < nks) at = mfma16(omk[j][ks], xf[ks], at);
+      } else if (arow) {  // precomputed A row (wide first layer): A[row lr][f0 + 4lq + r]
+        at = *reinterpret_cast<const f4*>(arow + f0 + 4 * lq);
       } else {
-        p0[r] = cl * fmaxf(at[r], 0.f);
-        p1[r] = 0.f;
+        const int fa = f0 + lr;
+        for (int ks = 0; ks < nks; ++ks) {
+          const int k = 4 * ks + lq;
+          const float o = (fa < R && k < d) ? om[(int64_t)k * R + fa] : 0.f;
+          at = mfma16(o, xs[lr * xst + 4 * ks + lq], at);
+        }
       }
-    }
-    float wcur[NOT][4][2];
-#pragma unroll
-    for (int ot = 0; ot < NOT; ++ot)
+      float p0[4], p1[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        wcur[ot][r][0] = wf[ot][r][0];
-        wcur[ot][r][1] = wf[ot][r][1];
+        if (RBF) {
+          float sn, cs;
+          rf_sincos(at[r], &sn, &cs);
+          p0[r] = cl * cs;
+          p1[r] = cl * sn;
+        } else {
+          p0[r] = cl * fmaxf(at[r], 0.f);
+          p1[r] = 0.f;
+        }
       }
-    if (f0 + NW * 16 < R) load_frag(f0 + NW * 16);  // prefetch next chunk
-    if (G1) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        dot = fmaf(p0[r], wcur[0][r][0], dot);
-        if (RBF) dot = fmaf(p1[r], wcur[0][r][1], dot);
-      }
-    } else {
-#pragma unroll
-      for (int ot = 0; ot < NOT; ++ot)
+      if (G1) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          acc[ot] = mfma16(wcur[ot][r][0], p0[r], acc[ot]);
-          if (RBF) acs[ot] = mfma16(wcur[ot][r][1], p1[r], acs[ot]);
+          dot = fmaf(p0[r], wf[j][0][r][0], dot);
+          if (RBF) dot = fmaf(p1[r], wf[j][0][r][1], dot);
         }
+      } else {
+#pragma unroll
+        for (int ot = 0; ot < NOT; ++ot)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            acc[ot] = mfma16(wf[j][ot][r][0], p0[r], acc[ot]);
+            if (RBF) acs[ot] = mfma16(wf[j][ot][r][1], p1[r], acs[ot]);
+          }
+      }
     }
   }
   constexpr int GP = NOT * 16;
@@ -159,10 +163,11 @@ __device__ __forceinline__ void layer_partial(const float* __restrict__ om,
   }
 }
 
-// One workgroup = one 16-row tile; its 4 waves split each layer's RF features (16-feature chunks
-// w, w+4, ...) and the per-wave F partials are summed in LDS in wave order.
-template <bool SMALLD, int NOTMAX>
-__global__ __launch_bounds__(256) void k_forward_rows(
+// One workgroup = one 16-row tile; its NWR waves split each layer's RF features (16-feature chunks
+// w, w + NWR, ...) and the per-wave F partials are summed in LDS in wave order.  NWR = 16 (4 waves
+// per SIMD) for test sets too small to fill the chip with the one-wave-per-tile tile kernel.
+template <bool SMALLD, int NOTMAX, int NWR>
+__global__ __launch_bounds__(64 * NWR) void k_forward_rows(
     const dgprf_plan_t pl, const float* __restrict__ theta, const float* __restrict__ omega,
     const float* __restrict__ der, const float* __restrict__ X, const float* __restrict__ Y,
     const int y_cols, const int64_t n, const FOut fo, float* __restrict__ logp_out,
@@ -172,7 +177,7 @@ __global__ __launch_bounds__(256) void k_forward_rows(
   // rows [row_begin, row_end) of the n-row set; a0 = A_1 = X Omega_1 of those rows
   // ([row - row_begin][R_1], k_step_agemm) for a wide first layer, or nullptr
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const FwdLds LD = fwd_lds(pl);
+  const FwdLds LD = fwd_lds(pl, NWR);
   const int chain = blockIdx.y;
   const int64_t ochain = pl.hyp_per_chain ? (int64_t)chain * pl.omega_total : 0;
   const int64_t dchain = pl.hyp_per_chain ? (int64_t)chain * pl.der_total : 0;
@@ -207,7 +212,7 @@ __global__ __launch_bounds__(256) void k_forward_rows(
       // runtime (layer) -> compile-time body: output tiles, kernel kind, g == 1 VALU path; layers
       // with d <= 32 take the register-fragment path even when another layer is wide
 #define DGPRF_LP(SD, NT, RB, G1_) \
-  layer_partial<SD, NT, RB, G1_>(om, W, R, d, g, cl, xs, LD.xst, red, wave, lr, lq, arow)
+  layer_partial<SD, NT, RB, G1_, NWR>(om, W, R, d, g, cl, xs, LD.xst, red, wave, lr, lq, arow)
 #define DGPRF_LP_ALL(SD)                                                                        \
   do {                                                                                          \
     if (g == 1) {                                                                               \
@@ -239,7 +244,7 @@ __global__ __launch_bounds__(256) void k_forward_rows(
       const int r = e / g, o = e - r * g;
       float v = red[r * GP + o];
 #pragma unroll
-      for (int w = 1; w < NW; ++w) v += red[w * TR * GP + r * GP + o];
+      for (int w = 1; w < NWR; ++w) v += red[w * TR * GP + r * GP + o];
       ft[r * LD.ftst + o] = v;
       const int64_t b = row0 + r;
       if (out && b < row_end) out[b * g + o] = v;
@@ -951,10 +956,24 @@ ForwardCfg forward_cfg(const dgprf_plan_t& pl, int64_t n) {
             (int64_t)pl.d[0] * pl.n_rf[0] < ((int64_t)1 << 29);
   // tile kernel: d <= 32 (layer 0 exempt when wide0 and no input concatenation), g <= 64,
   // R % 4 == 0 in every layer
-  c.tiles = pl.fwd_path != DGPRF_FWD_ROWS && ((pl.d_in <= 32) || (c.wide0 && !pl.input_cat));
-  for (int l = 0; l < pl.n_layers; ++l)
-    c.tiles = c.tiles && (pl.d[l] <= 32 || (l == 0 && c.wide0)) && pl.n_gp[l] <= 64 &&
+  bool tile_ok = (pl.d_in <= 32) || (c.wide0 && !pl.input_cat);
+  bool small = true;  // d <= 32 and g <= 16 in every layer: the 16-wave row kernel applies
+  for (int l = 0; l < pl.n_layers; ++l) {
+    tile_ok = tile_ok && (pl.d[l] <= 32 || (l == 0 && c.wide0)) && pl.n_gp[l] <= 64 &&
               pl.n_rf[l] % 4 == 0 && (int64_t)2 * pl.n_rf[l] * pl.n_gp[l] < ((int64_t)1 << 29);
+    small = small && pl.d[l] <= 32 && pl.n_gp[l] <= 16;
+  }
+  // the tile kernel gives each 16-row tile ONE wave through all layers: below FWD_TILE_MIN_ROWS
+  // rows it leaves most SIMDs idle, and the row kernel with 16 waves per tile (each a sixteenth
+  // of every layer's features, F partials summed in LDS) covers the chip instead
+  constexpr int64_t FWD_TILE_MIN_ROWS = 16384;
+  const bool few = n < FWD_TILE_MIN_ROWS && small && !c.wide0;
+  switch (pl.fwd_path) {
+    case DGPRF_FWD_ROWS: c.tiles = false; c.rows_waves = 4; break;
+    case DGPRF_FWD_ROWS16: c.tiles = false; c.rows_waves = small ? 16 : 4; break;
+    case DGPRF_FWD_TILE: c.tiles = tile_ok; c.rows_waves = 4; break;
+    default: c.tiles = tile_ok && !few; c.rows_waves = few ? 16 : 4; break;
+  }
   // chunks are whole 64-row tile-kernel workgroups: every wave of the last workgroup reads its 16
   // A_1 rows (rows past n included, their outputs discarded), so the scratch covers align64 rows
   const int64_t R0 = pl.n_rf[0];
@@ -973,7 +992,6 @@ hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const
                                float* lse_m, float* lse_s, float* se_sum, float* scratch,
                                hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  const FwdLds LD = fwd_lds(pl);
   FOut fo;
   for (int l = 0; l < DGPRF_MAX_LAYERS; ++l) fo.p[l] = (f_out && l < pl.n_layers) ? f_out[l] : nullptr;
   bool smalld = true;
@@ -1037,15 +1055,19 @@ hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const
 #undef DGPRF_TILE_LAUNCH
 #undef DGPRF_TILE_LAUNCH1
     } else {
-      const size_t lds = (size_t)LD.total * sizeof(float);
+      const int nwr = cfg.rows_waves;
+      const size_t lds = (size_t)fwd_lds(pl, nwr).total * sizeof(float);
       dim3 grid((unsigned)((nr + TR - 1) / TR), pl.n_chains);
-#define DGPRF_FWD_LAUNCH(S, NM)                                                                    \
+#define DGPRF_FWD_LAUNCH_W(S, NM, NWR_)                                                             \
   do {                                                                                             \
-    set_lds_limit((const void*)k_forward_rows<S, NM>, lds);                                        \
-    hipLaunchKernelGGL((k_forward_rows<S, NM>), grid, dim3(256), lds, s, pl, theta, omega, der, X, \
-                       Y, y_cols, n, fo, logp, se, lse_m, lse_s, se_sum, a0, r0, r1);             \
+    set_lds_limit((const void*)k_forward_rows<S, NM, NWR_>, lds);                                  \
+    hipLaunchKernelGGL((k_forward_rows<S, NM, NWR_>), grid, dim3(64 * NWR_), lds, s, pl, theta,    \
+                       omega, der, X, Y, y_cols, n, fo, logp, se, lse_m, lse_s, se_sum, a0, r0, r1); \
   } while (0)
-      if (smalld) {
+#define DGPRF_FWD_LAUNCH(S, NM) DGPRF_FWD_LAUNCH_W(S, NM, 4)
+      if (smalld && nwr == 16) {  // g <= 16 (forward_cfg)
+        DGPRF_FWD_LAUNCH_W(true, 1, 16);
+      } else if (smalld) {
         if (notmax == 1) DGPRF_FWD_LAUNCH(true, 1);
         else if (notmax == 2) DGPRF_FWD_LAUNCH(true, 2);
         else DGPRF_FWD_LAUNCH(true, 4);
@@ -1055,6 +1077,7 @@ hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const
         else DGPRF_FWD_LAUNCH(false, 4);
       }
 #undef DGPRF_FWD_LAUNCH
+#undef DGPRF_FWD_LAUNCH_W
     }
     err = hipGetLastError();
   }

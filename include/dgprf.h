@@ -73,8 +73,10 @@ extern "C" {
  * path for parity tests: the general row kernel, or a wide first layer contracted inside the forward
  * kernel instead of by the separate A_1 = X Omega_1 GEMM. */
 #define DGPRF_FWD_AUTO 0
-#define DGPRF_FWD_ROWS 1
+#define DGPRF_FWD_ROWS 1        /* row kernel, 4 waves per 16-row tile */
 #define DGPRF_FWD_NO_AGEMM 2
+#define DGPRF_FWD_TILE 3        /* tile kernel (one wave per 16-row tile) whatever the row count */
+#define DGPRF_FWD_ROWS16 4      /* row kernel, 16 waves per 16-row tile (small test sets) */
 
 /* error codes */
 #define DGPRF_OK 0

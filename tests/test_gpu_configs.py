@@ -93,6 +93,22 @@ def test_config_forward_and_grad(dev, cfg):
         assert rel_err(G[l], ref[l]) < 2e-4, (cfg, l)
 
 
+@pytest.mark.parametrize("path", ["tile", "rows16", "rows"])
+def test_predictive_paths_small_test_set(dev, path):
+    """Config 3's model on 1,001 test rows (a ragged tile) through the tile kernel (one wave per
+    16-row tile), the 16-wave row kernel (the product choice below 16k rows) and the 4-wave row
+    kernel: per-row log p against the oracle."""
+    from dgprf import _native as N
+    c = CONFIGS[3]
+    m, p = _model(c, 33)
+    Xt, Yt = _data(c, 1001, 203)
+    m._engine.set_forward_path({"tile": N.FWD_TILE, "rows16": N.FWD_ROWS16,
+                                "rows": N.FWD_ROWS}[path])
+    lp = cpu(m._engine.forward(Xt, Yt, logp=True)["logp"][0])
+    ref = O.log_prob(p, O.forward(p, Xt), Yt)
+    assert np.max(np.abs(lp - ref)) < 2e-5 * max(1.0, np.max(np.abs(ref)))
+
+
 def test_predictive_multi_round_rows(dev):
     """Config 2's shape (3-layer RBF, n_rf 1024, g [8,8,1]) over 70,001 test rows: more tiles than
     one round of resident waves (65,536 rows on 256 CUs) plus a ragged remainder; per-row log p
