@@ -192,13 +192,13 @@ __device__ __forceinline__ float sum_slices(const float* __restrict__ p, int64_t
   return acc;
 }
 
-__host__ __device__ inline void step_lds(int d, int g, LayerK& a, int& total) {
+__host__ __device__ inline void step_lds(int d, int g, LayerK& a, int& total, int nwb = NW) {
   a.xst = round4(d) + 1;
   a.aux_off = round4(TR * a.xst);
   a.auxst = g + 1;
   a.red_off = a.aux_off + 2 * round4(TR * a.auxst);  // dF tile + Y tile
   // backward: the workgroup's 64-feature block of W_l ([2][64*g] raw) and Omega_l ([64][OST])
-  a.stg_off = a.red_off + NW * TR * 64;
+  a.stg_off = a.red_off + nwb * TR * 64;  // per-wave reduction rows of nwb waves
   a.os_off = a.stg_off + (2 * 64 * g > 2048 ? round4(2 * 64 * g) : 2048);
   total = a.os_off + 64 * OST;
 }
@@ -284,6 +284,7 @@ __device__ __forceinline__ void elem_prologue(const LayerK& a, int chain, int ro
                                              float* scratch) {
   const int total = TR * round4(a.d) + nd_tile;
   const int t = threadIdx.x;
+  if (t >= 256) return;  // 8-wave workgroups: waves 0-3 own the elements (wave-uniform)
   const int wave0 = __builtin_amdgcn_readfirstlane(t & ~63);
   Elem e0, e1;
   if (wave0 < total) elem_issue(a, chain, row0, t, nd_tile, dfst, e0);
@@ -582,7 +583,7 @@ __global__ __launch_bounds__(256) void k_layer_update(const LayerK a) {
 // other workgroup of the slice has read the old values by then (its ticket follows its loads), so
 // no workgroup can see a half-updated slice.  Every workgroup of the slice computes bit-identical
 // values (same inputs, same order, same Philox counters).
-template <int KS, int NOT, bool RBF, bool G1, bool PEND>
+template <int KS, int NOT, bool RBF, bool G1, bool PEND, int NWB>
 // Minimum waves per SIMD the register allocation must allow.  Single-chain steps run one workgroup
 // per CU either way; with C chains per launch (13 x 16 x C workgroups) residency sets throughput:
 // the g <= 16, d <= 8 W-only backward at <= 168 VGPRs (3 waves/SIMD) measured 127k -> 156k
@@ -592,7 +593,7 @@ template <int KS, int NOT, bool RBF, bool G1, bool PEND>
 #ifndef DGPRF_STEP_WPE
 #define DGPRF_STEP_WPE 3
 #endif
-__global__ __launch_bounds__(256) void k_step_fwd(const LayerK a) {
+__global__ __launch_bounds__(64 * NWB) void k_step_fwd(const LayerK a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   int rt, sl;
   if (!tile_of_block(a, rt, sl)) return;
@@ -606,7 +607,9 @@ __global__ __launch_bounds__(256) void k_step_fwd(const LayerK a) {
   float* xs = smem;
   float* red = smem + a.red_off;
   const float* __restrict__ W = a.W + (int64_t)chain * a.w_cs;
-  auto chunk_f0 = [&](int i) { return ((sl * cpw + i) * NW + wave) * 16; };
+  // the slice's 4 cpw 16-feature chunks: iteration i of wave w takes chunk i NWB + w
+  auto chunk_f0 = [&](int i) { return ((sl * cpw * 4 + i * NWB) + wave) * 16; };
+  const int nit = cpw * 4 / NWB;
 
   // PEND: old theta / momenta / gW partials of the slice, issued first (up to 4 quads per thread)
   constexpr int PQ = PEND ? 4 : 1;
@@ -681,7 +684,7 @@ __global__ __launch_bounds__(256) void k_step_fwd(const LayerK a) {
   for (int ot = 0; ot < NOT; ++ot) acc[ot] = acs[ot] = f4zero();
   float acc1 = 0.f;  // G1: per-lane partial of F[row lr]
   DGPRF_STAMP(stamp_base, 6);
-  for (int i = 0; i < cpw; ++i) {
+  for (int i = 0; i < nit; ++i) {
     const int f0 = chunk_f0(i);
     if (f0 >= R) break;
     const f4 at = (KS == 0 && a0) ? *reinterpret_cast<const f4*>(a0 + f0 + 4 * lq)
@@ -697,7 +700,7 @@ __global__ __launch_bounds__(256) void k_step_fwd(const LayerK a) {
         wc[ot][r][0] = keep(wf[ot][r][0], ok);
         wc[ot][r][1] = keep(wf[ot][r][1], ok);
       }
-    if (i + 1 < cpw) {  // prefetch the next chunk (clamped loads are always in range)
+    if (i + 1 < nit) {  // prefetch the next chunk (clamped loads are always in range)
       if (KS > 0) load_om_frag<KS>(om, R, d, chunk_f0(i + 1), lr, lq, omk);
       if (PEND) load_w_frag_lds<NOT, RBF, G1>(pw, nhalf, R, g, fb0, chunk_f0(i + 1), lr, lq, wf);
       else load_w_frag<NOT, RBF, G1>(W, R, g, chunk_f0(i + 1), lr, lq, wf);
@@ -742,7 +745,7 @@ __global__ __launch_bounds__(256) void k_step_fwd(const LayerK a) {
     if (b < B) {
       float v = red[r * GP + o];
 #pragma unroll
-      for (int w = 1; w < NW; ++w) v += red[w * TR * GP + r * GP + o];
+      for (int w = 1; w < NWB; ++w) v += red[w * TR * GP + r * GP + o];
       fp[(int64_t)b * g + o] = v;
     }
   }
@@ -779,13 +782,13 @@ __device__ __forceinline__ void stage_slice_lds(const LayerK& a, const float* W,
   for (int h = 0; h < nh; ++h) {
     const float* src = W + ((int64_t)h * R + fb0) * g;
     float* dst = smem + a.wsa_off + h * nf * g;
-    for (int i0 = wave * 64; i0 < n4; i0 += 256) {
+    for (int i0 = wave * 64; i0 < n4; i0 += (int)blockDim.x) {
       if (i0 + lane < n4)
         __builtin_amdgcn_global_load_lds(src + 4 * (i0 + lane), dst + 4 * i0, 16, 0, 0);
     }
   }
   const int per_row = nf / 256;  // 256-float instructions per Omega row (cpw >= 4)
-  for (int j = wave; j < a.dxw * per_row; j += 4) {
+  for (int j = wave; j < a.dxw * per_row; j += (int)(blockDim.x >> 6)) {
     const int k = j / per_row, c = j - k * per_row;
     __builtin_amdgcn_global_load_lds(om + (int64_t)k * R + fb0 + c * 256 + 4 * lane,
                                      smem + a.osa_off + k * a.osa_st + c * 256, 16, 0, 0);
@@ -793,8 +796,8 @@ __device__ __forceinline__ void stage_slice_lds(const LayerK& a, const float* W,
 }
 
 
-template <int KS, int NOT, bool RBF, bool G1, bool FB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NOT == 1 && !FB && (KS == 1 || KS == 2 || (KS == 4 && !RBF))) ? DGPRF_STEP_WPE : 1))) void k_step_bwd(const LayerK a) {
+template <int KS, int NOT, bool RBF, bool G1, bool FB, int NWB>
+__global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT == 1 && !FB && (KS == 1 || KS == 2 || (KS == 4 && !RBF))) ? DGPRF_STEP_WPE : 1))) void k_step_bwd(const LayerK a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   if ((int)blockIdx.x >= a.main_blocks) {  // fused update of W_{l+2} / next-batch gather
     bwd_extra_block(a, (int)blockIdx.x - a.main_blocks, (int)blockIdx.z);
@@ -814,7 +817,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NOT == 1 &
   const int dfst = a.auxst;
   float* red = smem + a.red_off;
   const float* __restrict__ W = a.W + (int64_t)chain * a.w_cs;
-  auto chunk_f0 = [&](int i) { return ((sl * cpw + i) * NW + wave) * 16; };
+  // iteration i of wave w takes chunk i NWB + w of the slice (8-wave workgroups: whole-slice
+  // staging only, a.wstage)
+  auto chunk_f0 = [&](int i) { return ((sl * cpw * 4 + i * NWB) + wave) * 16; };
+  const int nit = cpw * 4 / NWB;
   constexpr int KGM = 4 * NOT;  // k-steps of the dPhi contraction (K = g)
   const int ND = (dxw + 15) >> 4;
   // dPhi / dA are needed for dX (l > 0) and, with full_bayesian=True, for every layer
@@ -1005,7 +1011,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NOT == 1 &
   float ampl = 0.f;
   if (FB)
     for (int e = lane; e < hst; e += 64) hw[e] = 0.f;
-  for (int i = 0; i < cpw; ++i) {
+  for (int i = 0; i < nit; ++i) {
     const int f0 = chunk_f0(i);
     if (f0 >= R) break;
     if (i > 0) {
@@ -1027,9 +1033,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NOT == 1 &
     float wd0[KGM], wd1[KGM];
     f4 oxv[4];
     // this chunk's 64-feature block: the per-chunk staging buffers, or its rows of the slice image
-    const float* wsc = a.wstage ? smem + a.wsa_off + i * 64 * g : wsl;
+    const float* wsc = a.wstage ? smem + a.wsa_off + i * NWB * 16 * g : wsl;
     const int whalf = a.wstage ? 64 * cpw * g : nwh;
-    const float* osc = a.wstage ? smem + a.osa_off + i * 64 : osl;
+    const float* osc = a.wstage ? smem + a.osa_off + i * NWB * 16 : osl;
     const int ostc = a.wstage ? a.osa_st : OST;
     if (dphi) {
       const bool frow = f0 + lr < R;
@@ -1196,7 +1202,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NOT == 1 &
     float* hp = a.hp + (int64_t)chain * a.ws_cs + ((int64_t)rt * NSM + sl) * hst;
     const float* h0 = smem + a.hred_off;
     for (int e = threadIdx.x; e < 2 * d + 1; e += blockDim.x)
-      hp[e] = ((h0[e] + h0[hst + e]) + h0[2 * hst + e]) + h0[3 * hst + e];
+      hp[e] = ((h0[e] + h0[hst + e]) + h0[2 * hst + e]) + h0[3 * hst + e];  // FB: NWB == 4
   }
   if (dxw > 0) {
     // dxa[dt][r] = dX[row lr][dt*16 + 4lq + r]; sum the 4 waves in LDS, store the slice partial.
@@ -1214,7 +1220,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NOT == 1 &
       if (b < B) {
         float v = red[r * DP + k];
 #pragma unroll
-        for (int w = 1; w < NW; ++w) v += red[w * TR * DP + r * DP + k];
+        for (int w = 1; w < NWB; ++w) v += red[w * TR * DP + r * DP + k];
         dxp[(int64_t)b * dxw + k] = v;
       }
     }
@@ -1763,7 +1769,7 @@ __global__ __launch_bounds__(256) void k_step_agemm(const AgemmK a) {
 }
 
 LayerK make_layer_k(const dgprf_plan_t& pl, const StepDev& sd, int l, int& lds_floats,
-                    bool bwd = false) {
+                    bool bwd = false, int nwb = NW) {
   LayerK a;
   const bool direct = sd.bd.mode == DGPRF_BATCH_DIRECT;
   // random_fixed=False layers read this step's Omega from the workspace (k_fresh_omega)
@@ -1798,7 +1804,7 @@ LayerK make_layer_k(const dgprf_plan_t& pl, const StepDev& sd, int l, int& lds_f
   a.last = l == pl.n_layers - 1;
   a.likelihood = pl.likelihood;
   a.layer = l;
-  step_lds(a.d, a.g, a, lds_floats);
+  step_lds(a.d, a.g, a, lds_floats, nwb);
   // element-owner prologue: X tile + dF tile <= 512 elements, W/Omega block staged by float4
   const int dpad = round4(a.d);
   a.ws = sd.ws;
@@ -1908,76 +1914,85 @@ void set_update_range(LayerK& a, const dgprf_plan_t& pl, int layer, int t_off) {
     else KERNEL##_launch2<0>(g, rbf, grid, lds, s, a);                                             \
   }
 
-// forward: KS x NOT x RBF x G1 (x PEND for the narrow layers the fused update covers: NOT == 1)
+// forward: KS x NOT x RBF x G1 (x PEND for the narrow layers the fused update covers: NOT == 1) x
+// waves per workgroup (8 for slices of >= 2 chunks per wave: two waves per SIMD hide each other's
+// MFMA / load latency; 4 otherwise and with PEND)
 template <int KS, int NOT, bool G1>
-void k_step_fwd_launch3(bool rbf, bool pend, dim3 grid, size_t lds, hipStream_t s, const LayerK& a) {
-#define DGPRF_FWD(R_, P_)                                                              \
-  do {                                                                                \
-    dgprf::set_lds_limit((const void*)k_step_fwd<KS, NOT, R_, G1, P_>, lds);         \
-    hipLaunchKernelGGL((k_step_fwd<KS, NOT, R_, G1, P_>), grid, dim3(256), lds, s, a); \
+void k_step_fwd_launch3(bool rbf, bool pend, bool w8, dim3 grid, size_t lds, hipStream_t s,
+                        const LayerK& a) {
+#define DGPRF_FWD(R_, P_, W_)                                                                  \
+  do {                                                                                        \
+    dgprf::set_lds_limit((const void*)k_step_fwd<KS, NOT, R_, G1, P_, W_>, lds);             \
+    hipLaunchKernelGGL((k_step_fwd<KS, NOT, R_, G1, P_, W_>), grid, dim3(64 * W_), lds, s, a); \
   } while (0)
   if (pend && NOT == 1) {
-    if (rbf) DGPRF_FWD(true, NOT == 1);
-    else DGPRF_FWD(false, NOT == 1);
+    if (rbf) DGPRF_FWD(true, NOT == 1, 4);
+    else DGPRF_FWD(false, NOT == 1, 4);
+  } else if (w8) {
+    if (rbf) DGPRF_FWD(true, false, 8);
+    else DGPRF_FWD(false, false, 8);
   } else {
-    if (rbf) DGPRF_FWD(true, false);
-    else DGPRF_FWD(false, false);
+    if (rbf) DGPRF_FWD(true, false, 4);
+    else DGPRF_FWD(false, false, 4);
   }
 #undef DGPRF_FWD
 }
 template <int KS>
-void k_step_fwd_launch2(int g, bool rbf, bool pend, dim3 grid, size_t lds, hipStream_t s,
+void k_step_fwd_launch2(int g, bool rbf, bool pend, bool w8, dim3 grid, size_t lds, hipStream_t s,
                         const LayerK& a) {
   const int NOT = (g + 15) >> 4;
-  if (g == 1) k_step_fwd_launch3<KS, 1, true>(rbf, pend, grid, lds, s, a);
-  else if (NOT == 1) k_step_fwd_launch3<KS, 1, false>(rbf, pend, grid, lds, s, a);
-  else if (NOT == 2) k_step_fwd_launch3<KS, 2, false>(rbf, false, grid, lds, s, a);
-  else if (NOT == 3) k_step_fwd_launch3<KS, 3, false>(rbf, false, grid, lds, s, a);
-  else k_step_fwd_launch3<KS, 4, false>(rbf, false, grid, lds, s, a);
+  if (g == 1) k_step_fwd_launch3<KS, 1, true>(rbf, pend, w8, grid, lds, s, a);
+  else if (NOT == 1) k_step_fwd_launch3<KS, 1, false>(rbf, pend, w8, grid, lds, s, a);
+  else if (NOT == 2) k_step_fwd_launch3<KS, 2, false>(rbf, false, w8, grid, lds, s, a);
+  else if (NOT == 3) k_step_fwd_launch3<KS, 3, false>(rbf, false, w8, grid, lds, s, a);
+  else k_step_fwd_launch3<KS, 4, false>(rbf, false, w8, grid, lds, s, a);
 }
-void k_step_fwd_launch(int d, int g, bool rbf, bool pend, dim3 grid, size_t lds, hipStream_t s,
-                       const LayerK& a) {
-  if (d <= 4) k_step_fwd_launch2<1>(g, rbf, pend, grid, lds, s, a);
-  else if (d <= 8) k_step_fwd_launch2<2>(g, rbf, pend, grid, lds, s, a);
-  else if (d <= 16) k_step_fwd_launch2<4>(g, rbf, pend, grid, lds, s, a);
-  else if (d <= 32) k_step_fwd_launch2<8>(g, rbf, pend, grid, lds, s, a);
-  else k_step_fwd_launch2<0>(g, rbf, false, grid, lds, s, a);
+void k_step_fwd_launch(int d, int g, bool rbf, bool pend, bool w8, dim3 grid, size_t lds,
+                       hipStream_t s, const LayerK& a) {
+  if (d <= 4) k_step_fwd_launch2<1>(g, rbf, pend, w8, grid, lds, s, a);
+  else if (d <= 8) k_step_fwd_launch2<2>(g, rbf, pend, w8, grid, lds, s, a);
+  else if (d <= 16) k_step_fwd_launch2<4>(g, rbf, pend, w8, grid, lds, s, a);
+  else if (d <= 32) k_step_fwd_launch2<8>(g, rbf, pend, w8, grid, lds, s, a);
+  else k_step_fwd_launch2<0>(g, rbf, false, w8, grid, lds, s, a);
 }
 
-// backward: KS x NOT x RBF x G1 x FB
+// backward: KS x NOT x RBF x G1 x FB x waves per workgroup (8: W-only with whole-slice staging)
 template <int KS, int NOT, bool G1>
-void k_step_bwd_launch3(bool rbf, bool fb, dim3 grid, size_t lds, hipStream_t s, const LayerK& a) {
-#define DGPRF_BWD(R_, F_)                                                             \
-  do {                                                                               \
-    dgprf::set_lds_limit((const void*)k_step_bwd<KS, NOT, R_, G1, F_>, lds);        \
-    hipLaunchKernelGGL((k_step_bwd<KS, NOT, R_, G1, F_>), grid, dim3(256), lds, s, a); \
+void k_step_bwd_launch3(bool rbf, bool fb, bool w8, dim3 grid, size_t lds, hipStream_t s,
+                        const LayerK& a) {
+#define DGPRF_BWD(R_, F_, W_)                                                                  \
+  do {                                                                                        \
+    dgprf::set_lds_limit((const void*)k_step_bwd<KS, NOT, R_, G1, F_, W_>, lds);             \
+    hipLaunchKernelGGL((k_step_bwd<KS, NOT, R_, G1, F_, W_>), grid, dim3(64 * W_), lds, s, a); \
   } while (0)
   if (rbf) {
-    if (fb) DGPRF_BWD(true, true);
-    else DGPRF_BWD(true, false);
+    if (fb) DGPRF_BWD(true, true, 4);
+    else if (w8) DGPRF_BWD(true, false, 8);
+    else DGPRF_BWD(true, false, 4);
   } else {
-    if (fb) DGPRF_BWD(false, true);
-    else DGPRF_BWD(false, false);
+    if (fb) DGPRF_BWD(false, true, 4);
+    else if (w8) DGPRF_BWD(false, false, 8);
+    else DGPRF_BWD(false, false, 4);
   }
 #undef DGPRF_BWD
 }
 template <int KS>
-void k_step_bwd_launch2(int g, bool rbf, bool fb, dim3 grid, size_t lds, hipStream_t s,
+void k_step_bwd_launch2(int g, bool rbf, bool fb, bool w8, dim3 grid, size_t lds, hipStream_t s,
                         const LayerK& a) {
   const int NOT = (g + 15) >> 4;
-  if (g == 1) k_step_bwd_launch3<KS, 1, true>(rbf, fb, grid, lds, s, a);
-  else if (NOT == 1) k_step_bwd_launch3<KS, 1, false>(rbf, fb, grid, lds, s, a);
-  else if (NOT == 2) k_step_bwd_launch3<KS, 2, false>(rbf, fb, grid, lds, s, a);
-  else if (NOT == 3) k_step_bwd_launch3<KS, 3, false>(rbf, fb, grid, lds, s, a);
-  else k_step_bwd_launch3<KS, 4, false>(rbf, fb, grid, lds, s, a);
+  if (g == 1) k_step_bwd_launch3<KS, 1, true>(rbf, fb, w8, grid, lds, s, a);
+  else if (NOT == 1) k_step_bwd_launch3<KS, 1, false>(rbf, fb, w8, grid, lds, s, a);
+  else if (NOT == 2) k_step_bwd_launch3<KS, 2, false>(rbf, fb, w8, grid, lds, s, a);
+  else if (NOT == 3) k_step_bwd_launch3<KS, 3, false>(rbf, fb, w8, grid, lds, s, a);
+  else k_step_bwd_launch3<KS, 4, false>(rbf, fb, w8, grid, lds, s, a);
 }
-void k_step_bwd_launch(int d, int g, bool rbf, bool fb, dim3 grid, size_t lds, hipStream_t s,
-                       const LayerK& a) {
-  if (d <= 4) k_step_bwd_launch2<1>(g, rbf, fb, grid, lds, s, a);
-  else if (d <= 8) k_step_bwd_launch2<2>(g, rbf, fb, grid, lds, s, a);
-  else if (d <= 16) k_step_bwd_launch2<4>(g, rbf, fb, grid, lds, s, a);
-  else if (d <= 32) k_step_bwd_launch2<8>(g, rbf, fb, grid, lds, s, a);
-  else k_step_bwd_launch2<0>(g, rbf, fb, grid, lds, s, a);
+void k_step_bwd_launch(int d, int g, bool rbf, bool fb, bool w8, dim3 grid, size_t lds,
+                       hipStream_t s, const LayerK& a) {
+  if (d <= 4) k_step_bwd_launch2<1>(g, rbf, fb, w8, grid, lds, s, a);
+  else if (d <= 8) k_step_bwd_launch2<2>(g, rbf, fb, w8, grid, lds, s, a);
+  else if (d <= 16) k_step_bwd_launch2<4>(g, rbf, fb, w8, grid, lds, s, a);
+  else if (d <= 32) k_step_bwd_launch2<8>(g, rbf, fb, w8, grid, lds, s, a);
+  else k_step_bwd_launch2<0>(g, rbf, fb, w8, grid, lds, s, a);
 }
 
 }  // namespace
@@ -1999,9 +2014,12 @@ namespace dgprf {
 
 hipError_t launch_step_fwd(const dgprf_plan_t& pl, const StepDev& sd, int layer, hipStream_t s,
                            const UpdateDev* ud, bool pend) {
-  int lds_floats = 0;
-  LayerK a = make_layer_k(pl, sd, layer, lds_floats);
   pend = pend && ud && layer == 0 && pl.fused_update && pl.n_gp[0] <= 16 && pl.d[0] <= 32;
+  // 8 waves per workgroup when every wave still gets >= 2 chunks and no pending update is applied
+  // (config 3, cpw = 2: one chunk per wave measured slower, 37.6 vs 35.9 us/step)
+  const bool w8 = !pend && pl.cpw[layer] >= 4 && pl.cpw[layer] % 2 == 0;
+  int lds_floats = 0;
+  LayerK a = make_layer_k(pl, sd, layer, lds_floats, false, w8 ? 8 : 4);
   if (pend) {  // the previous step's W_1 update, applied by this forward (its step offset - 1)
     fill_fused(a, pl, sd, *ud);
     a.pend = 1;
@@ -2027,15 +2045,23 @@ hipError_t launch_step_fwd(const dgprf_plan_t& pl, const StepDev& sd, int layer,
     hipLaunchKernelGGL(k_step_agemm, ggrid, dim3(256), 0, s, g);
   }
   dim3 grid(a.main_blocks, 1, pl.n_chains);
-  k_step_fwd_launch(pl.d[layer], pl.n_gp[layer], pl.kind[layer] == DGPRF_RBF, pend, grid,
+  k_step_fwd_launch(pl.d[layer], pl.n_gp[layer], pl.kind[layer] == DGPRF_RBF, pend, w8, grid,
                     (size_t)lds_floats * sizeof(float), s, a);
   return hipGetLastError();
 }
 
 hipError_t launch_step_bwd(const dgprf_plan_t& pl, const StepDev& sd, int layer, hipStream_t s,
                            const UpdateDev* ud, bool gather_next) {
+  // 8 waves per workgroup for W-only steps whose slices are staged whole (a.wstage; not with the
+  // fused update's extra workgroups, which assume 4)
+  bool w8 = !sd.full_bayes && !(ud && pl.fused_update) && pl.cpw[layer] % 4 == 0;
   int lds_floats = 0;
-  LayerK a = make_layer_k(pl, sd, layer, lds_floats, /*bwd=*/true);
+  LayerK a = make_layer_k(pl, sd, layer, lds_floats, /*bwd=*/true, w8 ? 8 : 4);
+  if (w8 && !a.wstage) {  // the slice image does not fit next to 8 waves' rows: 4 waves
+    w8 = false;
+    lds_floats = 0;
+    a = make_layer_k(pl, sd, layer, lds_floats, /*bwd=*/true, 4);
+  }
   if (ud && pl.fused_update) {
     fill_fused(a, pl, sd, *ud);
     // extra workgroups: W_{l+2}'s update from the gW partials layer l+1's backward just wrote
@@ -2051,8 +2077,7 @@ hipError_t launch_step_bwd(const dgprf_plan_t& pl, const StepDev& sd, int layer,
   }
   dim3 grid(a.main_blocks + a.upd_blocks + a.gat_blocks, 1, pl.n_chains);
   k_step_bwd_launch(pl.d[layer], pl.n_gp[layer], pl.kind[layer] == DGPRF_RBF, sd.full_bayes != 0,
-                    grid,
-                    (size_t)lds_floats * sizeof(float), s, a);
+                    w8, grid, (size_t)lds_floats * sizeof(float), s, a);
   return hipGetLastError();
 }
 
