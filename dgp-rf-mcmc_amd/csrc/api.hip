@@ -125,7 +125,8 @@ hipError_t enqueue_step(const dgprf_plan_t& pl, const StepDev& sd, const UpdateD
       e = dgprf::launch_step_fwd(pl, sd, l, s, &ud, l == 0 && pend0);
     for (int l = pl.n_layers - 1; l >= 0 && e == hipSuccess; --l)
       e = dgprf::launch_step_bwd(pl, sd, l, s, &ud, gather_next);
-    if (e == hipSuccess && !defer0) e = dgprf::launch_layer_update(pl, sd, ud, 0, s);
+    if (e == hipSuccess && !(defer0 && pl.fused_update == 1))
+      e = dgprf::launch_layer_update(pl, sd, ud, 0, s);
     return e;
   }
   for (int l = 0; l < pl.n_layers && e == hipSuccess; ++l) e = dgprf::launch_step_fwd(pl, sd, l, s);
@@ -283,13 +284,18 @@ int dgprf_plan_init(dgprf_plan_t* pl) {
   // fused update (W-only steps): layer 1's slice of W (both halves) fits the forward's LDS staging
   // (<= 4096 floats: 4 float4 per thread), whole float4 runs per half, <= 16 row tiles (one burst
   // of partial loads), a narrow first layer (no A_1 GEMM) and 32-bit buffer offsets
+  // 2: W_{l+2} by extra workgroups of layer l's backward, W_1 by its own small kernel each step;
+  // 1: as 2, and W_1's update can also wait for the next step's forward (its slice of W_1 fits
+  // the forward's LDS staging, <= 4096 floats; whole float4 runs per half; narrow layer 1)
   {
     const int h0 = pl->kind[0] == DGPRF_RBF ? 2 : 1;
     const int64_t slice = (int64_t)h0 * 64 * pl->cpw[0] * pl->n_gp[0];
-    pl->fused_update = pl->fuse_update == 1 && slice <= 4096 && pl->n_gp[0] <= 16 &&
-                       ((int64_t)pl->n_rf[0] * pl->n_gp[0]) % 4 == 0 && pl->n_row_tiles <= 16 &&
-                       pl->a0_off < 0 && pl->ws_chain * pl->n_chains < ((int64_t)1 << 29) &&
-                       pl->w_total * pl->n_chains < ((int64_t)1 << 29);
+    const bool ok = pl->fuse_update == 1 && pl->n_row_tiles <= 16 &&
+                    pl->ws_chain * pl->n_chains < ((int64_t)1 << 29) &&
+                    pl->w_total * pl->n_chains < ((int64_t)1 << 29);
+    const bool pend = slice <= 4096 && pl->n_gp[0] <= 16 &&
+                      ((int64_t)pl->n_rf[0] * pl->n_gp[0]) % 4 == 0 && pl->a0_off < 0;
+    pl->fused_update = ok ? (pend ? 1 : 2) : 0;
   }
   pl->initialised = 1;
   return DGPRF_OK;
@@ -375,7 +381,9 @@ int dgprf_graph_create_sghmc(dgprf_graph_handle* out, const dgprf_plan_t* plan,
     sd.full_bayes = st.full_bayes != 0;
     sd.xb_sel = fused ? (k & 1) : 0;
     const bool more = k + 1 < steps_per_graph;
-    e = enqueue_step(*plan, sd, ud, cs, k == 0, more, /*pend0=*/k > 0, /*defer0=*/more);
+    const bool defer = plan->fused_update == 1;  // W_1's update may wait for the next forward
+    e = enqueue_step(*plan, sd, ud, cs, k == 0, more, /*pend0=*/defer && k > 0,
+                     /*defer0=*/defer && more);
   }
   if (e == hipSuccess) e = dgprf::launch_advance(chain->step, steps_per_graph, cs);
   hipGraph_t g = nullptr;

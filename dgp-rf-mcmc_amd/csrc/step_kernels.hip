@@ -524,11 +524,11 @@ __device__ __forceinline__ f4 gw_partial_sum(rsrc_t rs, int64_t row_stride, int 
 }
 
 // ------------------------------------------------------------------------- fused update workgroups
-// One 256-thread workgroup's 1024 packed elements of the update of layer a.upd_layer's W from its
+// One workgroup's 4 x blockDim packed elements of the update of layer a.upd_layer's W from its
 // row-tile gW partials (written by an earlier kernel): extra workgroups of the next layer's
 // backward, or the flush kernel.
 __device__ __forceinline__ void update_layer_block(const LayerK& a, int j, int chain) {
-  const int64_t e0 = a.upd_lo + 4 * ((int64_t)j * 256 + threadIdx.x);
+  const int64_t e0 = a.upd_lo + 4 * ((int64_t)j * blockDim.x + threadIdx.x);
   if (e0 >= a.upd_hi) return;
   const int64_t cw = (int64_t)chain * a.w_cs;
   const f4 th = *reinterpret_cast<const f4*>(a.th0 + cw + e0);
@@ -563,11 +563,11 @@ __device__ __forceinline__ void bwd_extra_block(const LayerK& a, int j, int chai
   float* xb = a.xb_next + (int64_t)chain * a.ws_cs;
   float* yb = a.yb_next + (int64_t)chain * a.ws_cs;
   if (a.d_in > GATHER_WIDE) {  // one wave per row
-    const int b = j * 4 + (int)(threadIdx.x >> 6);
+    const int b = j * (int)(blockDim.x >> 6) + (int)(threadIdx.x >> 6);
     if (b < a.B) gather_row_wave(a.bd, a.B, a.d_in, a.yb_cols, xb, yb, chain, t, b, threadIdx.x & 63);
     return;
   }
-  const int b = j * 256 + (int)threadIdx.x;
+  const int b = j * (int)blockDim.x + (int)threadIdx.x;
   if (b < a.B) gather_row(a.bd, a.B, a.d_in, a.yb_cols, xb, yb, chain, t, b);
 }
 
@@ -796,13 +796,16 @@ __device__ __forceinline__ void stage_slice_lds(const LayerK& a, const float* W,
 }
 
 
-template <int KS, int NOT, bool RBF, bool G1, bool FB, int NWB>
+// NWB: waves per workgroup (8: W-only, whole-slice LDS image); FUSED: the fused update's extra
+// workgroups (own instantiations, so their registers never burden the plain kernels).
+template <int KS, int NOT, bool RBF, bool G1, bool FB, int NWB, bool FUSED>
 __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT == 1 && !FB && (KS == 1 || KS == 2 || (KS == 4 && !RBF))) ? DGPRF_STEP_WPE : 1))) void k_step_bwd(const LayerK a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  if ((int)blockIdx.x >= a.main_blocks) {  // fused update of W_{l+2} / next-batch gather
+  if (FUSED && (int)blockIdx.x >= a.main_blocks) {  // fused update of W_{l+2} / next-batch gather
     bwd_extra_block(a, (int)blockIdx.x - a.main_blocks, (int)blockIdx.z);
     return;
   }
+  constexpr bool WST = NWB == 8;  // whole-slice staging (a.wstage == 1 exactly then)
   int rt, sl;
   if (!tile_of_block(a, rt, sl)) return;
   const int chain = blockIdx.z;
@@ -888,8 +891,8 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
   if (a.fast) {
     // ---- single burst: W/Omega block, X tile, dF (or F_L) partials and Y rows
     f4 sw[2], so;
-    if (dphi && a.wstage) stage_slice_lds(a, W, om, fb0, smem);
-    if (dphi && !a.wstage) {
+    if (WST && dphi) stage_slice_lds(a, W, om, fb0, smem);
+    if (!WST && dphi) {
       const rsrc_t rw = make_rsrc(W, (int64_t)(RBF ? 2 : 1) * R * g);
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
@@ -903,15 +906,15 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
     }
     DGPRF_STAMP(stamp_base, 1);
     elem_prologue(a, chain, row0, TR * g, xs, dfs, dfst, ysh, red);
-    if (dphi && !a.wstage) {
+    if (!WST && dphi) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) *reinterpret_cast<f4*>(wsl + 4 * ((int)threadIdx.x + 256 * j)) = sw[j];
       *reinterpret_cast<f4*>(osl + (threadIdx.x >> 4) * OST + 4 * (threadIdx.x & 15)) = so;
     }
     DGPRF_STAMP(stamp_base, 4);
   } else {
-    if (dphi && a.wstage) stage_slice_lds(a, W, om, fb0, smem);
-    if (dphi && !a.wstage) stage_load(fb0);
+    if (WST && dphi) stage_slice_lds(a, W, om, fb0, smem);
+    if (!WST && dphi) stage_load(fb0);
     if (KS > 0 || !a.a0 || FB) load_x_tile(a, chain, row0, xs);
     for (int e = threadIdx.x; e < TR * g; e += blockDim.x) {  // dF (or F_L) slice sums; Y alongside
       const int r = e / g, o = e - r * g, b = row0 + r, bc = min(b, B - 1);
@@ -970,7 +973,7 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
       }
     }
   }
-  if (!a.fast && dphi && !a.wstage) stage_store(fb0);
+  if (!WST && !a.fast && dphi) stage_store(fb0);
   __syncthreads();
   DGPRF_STAMP(stamp_base, 2);
 
@@ -1019,7 +1022,7 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
       if (FB)
 #pragma unroll
         for (int dt = 0; dt < NZ; ++dt) zpf[dt] = z_frag(f0, dt);
-      if (dphi && !a.wstage) {
+      if (!WST && dphi) {
         stage_load((sl * cpw + i) * 64);
         __syncthreads();  // every wave is done with the previous block
         stage_store((sl * cpw + i) * 64);
@@ -1033,10 +1036,10 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
     float wd0[KGM], wd1[KGM];
     f4 oxv[4];
     // this chunk's 64-feature block: the per-chunk staging buffers, or its rows of the slice image
-    const float* wsc = a.wstage ? smem + a.wsa_off + i * NWB * 16 * g : wsl;
-    const int whalf = a.wstage ? 64 * cpw * g : nwh;
-    const float* osc = a.wstage ? smem + a.osa_off + i * NWB * 16 : osl;
-    const int ostc = a.wstage ? a.osa_st : OST;
+    const float* wsc = WST ? smem + a.wsa_off + i * NWB * 16 * g : wsl;
+    const int whalf = WST ? 64 * cpw * g : nwh;
+    const float* osc = WST ? smem + a.osa_off + i * NWB * 16 : osl;
+    const int ostc = WST ? a.osa_st : OST;
     if (dphi) {
       const bool frow = f0 + lr < R;
 #pragma unroll
@@ -1832,7 +1835,7 @@ LayerK make_layer_k(const dgprf_plan_t& pl, const StepDev& sd, int l, int& lds_f
     const int nf = 64 * a.cpw, nh = a.kind_rbf ? 2 : 1;
     const int wsa = a.stg_off, osa = wsa + round4(nh * nf * a.g), ost = nf + 4;
     const int end = osa + a.dxw * ost + (sd.full_bayes ? NW * round4(2 * a.d + 1) : 0);
-    if (bwd && a.cpw % 4 == 0 && a.R % nf == 0 && ((int64_t)a.R * a.g) % 4 == 0 &&
+    if (bwd && nwb == 8 && a.cpw % 4 == 0 && a.R % nf == 0 && ((int64_t)a.R * a.g) % 4 == 0 &&
         end <= 38 * 1024) {
       a.wstage = 1;
       a.wsa_off = wsa;
@@ -1873,12 +1876,12 @@ void fill_fused(LayerK& a, const dgprf_plan_t& pl, const StepDev& sd, const Upda
   a.ud = ud;
 }
 
-// Layer `layer`'s packed W range for the update workgroups.
-void set_update_range(LayerK& a, const dgprf_plan_t& pl, int layer, int t_off) {
+// Layer `layer`'s packed W range for the update workgroups of `threads` threads.
+void set_update_range(LayerK& a, const dgprf_plan_t& pl, int layer, int t_off, int threads = 256) {
   a.upd_layer = layer;
   a.upd_lo = (int32_t)pl.w_off[layer];
   a.upd_hi = (int32_t)(pl.w_off[layer] + (int64_t)pl.P[layer] * pl.n_gp[layer]);
-  a.upd_blocks = (a.upd_hi - a.upd_lo + 1023) / 1024;
+  a.upd_blocks = (a.upd_hi - a.upd_lo + 4 * threads - 1) / (4 * threads);
   a.upd_t_off = t_off;
 }
 
@@ -1957,42 +1960,45 @@ void k_step_fwd_launch(int d, int g, bool rbf, bool pend, bool w8, dim3 grid, si
 }
 
 // backward: KS x NOT x RBF x G1 x FB x waves per workgroup (8: W-only with whole-slice staging)
+// x FUSED (W-only, 4 waves)
 template <int KS, int NOT, bool G1>
-void k_step_bwd_launch3(bool rbf, bool fb, bool w8, dim3 grid, size_t lds, hipStream_t s,
+void k_step_bwd_launch3(bool rbf, bool fb, bool w8, bool fu, dim3 grid, size_t lds, hipStream_t s,
                         const LayerK& a) {
-#define DGPRF_BWD(R_, F_, W_)                                                                  \
-  do {                                                                                        \
-    dgprf::set_lds_limit((const void*)k_step_bwd<KS, NOT, R_, G1, F_, W_>, lds);             \
-    hipLaunchKernelGGL((k_step_bwd<KS, NOT, R_, G1, F_, W_>), grid, dim3(64 * W_), lds, s, a); \
+#define DGPRF_BWD(R_, F_, W_, U_)                                                                 \
+  do {                                                                                           \
+    dgprf::set_lds_limit((const void*)k_step_bwd<KS, NOT, R_, G1, F_, W_, U_>, lds);            \
+    hipLaunchKernelGGL((k_step_bwd<KS, NOT, R_, G1, F_, W_, U_>), grid, dim3(64 * W_), lds, s, a); \
   } while (0)
   if (rbf) {
-    if (fb) DGPRF_BWD(true, true, 4);
-    else if (w8) DGPRF_BWD(true, false, 8);
-    else DGPRF_BWD(true, false, 4);
+    if (fb) DGPRF_BWD(true, true, 4, false);
+    else if (fu) DGPRF_BWD(true, false, 4, true);
+    else if (w8) DGPRF_BWD(true, false, 8, false);
+    else DGPRF_BWD(true, false, 4, false);
   } else {
-    if (fb) DGPRF_BWD(false, true, 4);
-    else if (w8) DGPRF_BWD(false, false, 8);
-    else DGPRF_BWD(false, false, 4);
+    if (fb) DGPRF_BWD(false, true, 4, false);
+    else if (fu) DGPRF_BWD(false, false, 4, true);
+    else if (w8) DGPRF_BWD(false, false, 8, false);
+    else DGPRF_BWD(false, false, 4, false);
   }
 #undef DGPRF_BWD
 }
 template <int KS>
-void k_step_bwd_launch2(int g, bool rbf, bool fb, bool w8, dim3 grid, size_t lds, hipStream_t s,
-                        const LayerK& a) {
+void k_step_bwd_launch2(int g, bool rbf, bool fb, bool w8, bool fu, dim3 grid, size_t lds,
+                        hipStream_t s, const LayerK& a) {
   const int NOT = (g + 15) >> 4;
-  if (g == 1) k_step_bwd_launch3<KS, 1, true>(rbf, fb, w8, grid, lds, s, a);
-  else if (NOT == 1) k_step_bwd_launch3<KS, 1, false>(rbf, fb, w8, grid, lds, s, a);
-  else if (NOT == 2) k_step_bwd_launch3<KS, 2, false>(rbf, fb, w8, grid, lds, s, a);
-  else if (NOT == 3) k_step_bwd_launch3<KS, 3, false>(rbf, fb, w8, grid, lds, s, a);
-  else k_step_bwd_launch3<KS, 4, false>(rbf, fb, w8, grid, lds, s, a);
+  if (g == 1) k_step_bwd_launch3<KS, 1, true>(rbf, fb, w8, fu, grid, lds, s, a);
+  else if (NOT == 1) k_step_bwd_launch3<KS, 1, false>(rbf, fb, w8, fu, grid, lds, s, a);
+  else if (NOT == 2) k_step_bwd_launch3<KS, 2, false>(rbf, fb, w8, fu, grid, lds, s, a);
+  else if (NOT == 3) k_step_bwd_launch3<KS, 3, false>(rbf, fb, w8, fu, grid, lds, s, a);
+  else k_step_bwd_launch3<KS, 4, false>(rbf, fb, w8, fu, grid, lds, s, a);
 }
-void k_step_bwd_launch(int d, int g, bool rbf, bool fb, bool w8, dim3 grid, size_t lds,
+void k_step_bwd_launch(int d, int g, bool rbf, bool fb, bool w8, bool fu, dim3 grid, size_t lds,
                        hipStream_t s, const LayerK& a) {
-  if (d <= 4) k_step_bwd_launch2<1>(g, rbf, fb, w8, grid, lds, s, a);
-  else if (d <= 8) k_step_bwd_launch2<2>(g, rbf, fb, w8, grid, lds, s, a);
-  else if (d <= 16) k_step_bwd_launch2<4>(g, rbf, fb, w8, grid, lds, s, a);
-  else if (d <= 32) k_step_bwd_launch2<8>(g, rbf, fb, w8, grid, lds, s, a);
-  else k_step_bwd_launch2<0>(g, rbf, fb, w8, grid, lds, s, a);
+  if (d <= 4) k_step_bwd_launch2<1>(g, rbf, fb, w8, fu, grid, lds, s, a);
+  else if (d <= 8) k_step_bwd_launch2<2>(g, rbf, fb, w8, fu, grid, lds, s, a);
+  else if (d <= 16) k_step_bwd_launch2<4>(g, rbf, fb, w8, fu, grid, lds, s, a);
+  else if (d <= 32) k_step_bwd_launch2<8>(g, rbf, fb, w8, fu, grid, lds, s, a);
+  else k_step_bwd_launch2<0>(g, rbf, fb, w8, fu, grid, lds, s, a);
 }
 
 }  // namespace
@@ -2014,7 +2020,7 @@ namespace dgprf {
 
 hipError_t launch_step_fwd(const dgprf_plan_t& pl, const StepDev& sd, int layer, hipStream_t s,
                            const UpdateDev* ud, bool pend) {
-  pend = pend && ud && layer == 0 && pl.fused_update && pl.n_gp[0] <= 16 && pl.d[0] <= 32;
+  pend = pend && ud && layer == 0 && pl.fused_update == 1 && pl.n_gp[0] <= 16 && pl.d[0] <= 32;
   // 8 waves per workgroup when every wave still gets >= 2 chunks and no pending update is applied
   // (config 3, cpw = 2: one chunk per wave measured slower, 37.6 vs 35.9 us/step)
   const bool w8 = !pend && pl.cpw[layer] >= 4 && pl.cpw[layer] % 2 == 0;
@@ -2052,9 +2058,10 @@ hipError_t launch_step_fwd(const dgprf_plan_t& pl, const StepDev& sd, int layer,
 
 hipError_t launch_step_bwd(const dgprf_plan_t& pl, const StepDev& sd, int layer, hipStream_t s,
                            const UpdateDev* ud, bool gather_next) {
-  // 8 waves per workgroup for W-only steps whose slices are staged whole (a.wstage; not with the
-  // fused update's extra workgroups, which assume 4)
-  bool w8 = !sd.full_bayes && !(ud && pl.fused_update) && pl.cpw[layer] % 4 == 0;
+  // 8 waves per workgroup for W-only steps whose slices are staged whole (a.wstage); not with the
+  // fused update's extra workgroups (measured slower)
+  const bool fused = ud && pl.fused_update;
+  bool w8 = !sd.full_bayes && !fused && pl.cpw[layer] % 4 == 0;
   int lds_floats = 0;
   LayerK a = make_layer_k(pl, sd, layer, lds_floats, /*bwd=*/true, w8 ? 8 : 4);
   if (w8 && !a.wstage) {  // the slice image does not fit next to 8 waves' rows: 4 waves
@@ -2062,13 +2069,15 @@ hipError_t launch_step_bwd(const dgprf_plan_t& pl, const StepDev& sd, int layer,
     lds_floats = 0;
     a = make_layer_k(pl, sd, layer, lds_floats, /*bwd=*/true, 4);
   }
-  if (ud && pl.fused_update) {
+  if (fused) {
     fill_fused(a, pl, sd, *ud);
     // extra workgroups: W_{l+2}'s update from the gW partials layer l+1's backward just wrote
-    if (layer + 1 < pl.n_layers) set_update_range(a, pl, layer + 1, sd.step_offset);
+    const int nt = 256;
+    if (layer + 1 < pl.n_layers) set_update_range(a, pl, layer + 1, sd.step_offset, nt);
     // and, in the last layer's backward, step t+1's rows into the other buffer
     if (gather_next && layer == pl.n_layers - 1 && sd.bd.mode == DGPRF_BATCH_EPOCH) {
-      a.gat_blocks = pl.d_in > GATHER_WIDE ? (pl.batch + 3) / 4 : (pl.batch + 255) / 256;
+      a.gat_blocks = pl.d_in > GATHER_WIDE ? (pl.batch + nt / 64 - 1) / (nt / 64)
+                                           : (pl.batch + nt - 1) / nt;
       a.bd = sd.bd;
       a.xb_next = sd.ws + (sd.xb_sel ? pl.xb_off : pl.xb_alt_off);
       a.yb_next = sd.ws + (sd.xb_sel ? pl.yb_off : pl.yb_alt_off);
@@ -2077,7 +2086,7 @@ hipError_t launch_step_bwd(const dgprf_plan_t& pl, const StepDev& sd, int layer,
   }
   dim3 grid(a.main_blocks + a.upd_blocks + a.gat_blocks, 1, pl.n_chains);
   k_step_bwd_launch(pl.d[layer], pl.n_gp[layer], pl.kind[layer] == DGPRF_RBF, sd.full_bayes != 0,
-                    w8, grid, (size_t)lds_floats * sizeof(float), s, a);
+                    w8, fused, grid, (size_t)lds_floats * sizeof(float), s, a);
   return hipGetLastError();
 }
 

@@ -154,13 +154,12 @@ typedef struct dgprf_plan {
   int64_t xb_off;                    /* gathered minibatch rows X [B][d_in] (per chain)        */
   int64_t yb_off;                    /* gathered minibatch targets [B][yb_cols] (per chain)    */
   int32_t yb_cols;                   /* g_L (Gaussian) or 1 (softmax label)                    */
-  int32_t fused_update;              /* fuse_update granted (the shapes allow it; measured no
-                                        faster on config 2, DESIGN.md §4, so off by default).
-                                        1: W-only steps apply the SGHMC update inside the forward
-                                        / backward kernels (no separate update launch): W_{l+1} by
-                                        extra workgroups of layer l's backward, W_1 deferred into the
-                                        next step's layer-1 forward (or a flush kernel at the end of
-                                        a call / graph).  0: the update kernel runs per step.     */
+  int32_t fused_update;              /* fuse_update granted for W-only steps (0: one update kernel
+                                        per step).  2: W_{l+2} updated by extra workgroups of layer
+                                        l's backward, W_1 by its own small kernel per step.  1: as 2,
+                                        and in graphs W_1's update is deferred into the next step's
+                                        layer-1 forward (its slice fits the forward's LDS), with a
+                                        flush kernel at the end of a call / graph.               */
   int64_t a0_off;                    /* layer 1 with d > 32 (e.g. the 784-wide MNIST input):
                                         A_1 = X Omega_1 [align32(B)][R_1] precomputed by one tiled
                                         MFMA GEMM per step (per chain); -1 when not used          */
