@@ -105,9 +105,9 @@ def cpu_baseline(seconds):
 
 def pmc_traffic(prefix):
     """HBM-side bytes per launch of the kernels named `prefix...` (dispatch-weighted mean), from the
-    committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes (profiles/r01b/pmc_traffic.json, made by
+    committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes (profiles/r02/pmc_traffic.json, made by
     scripts/gpu_profile_round.sh; FETCH doubled per MI355X_MICROARCH.md §HBM).  None if absent."""
-    path = os.path.join(ROOT, "profiles", "r01b", "pmc_traffic.json")
+    path = os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json")
     if not os.path.exists(path):
         return None
     with open(path) as fh:
@@ -172,6 +172,7 @@ def bench_config(cfg, dev, rank, world, barrier_sync, max_over_ranks, steps):
            "steps_per_s": round(world * steps / t_s, 1),
            "us_per_step": round(t_s * 1e6 / steps, 2),
            "step_mflop": round((sum(fwd_f) + sum(bwd_f)) / 1e6, 2),
+           "step_mfma_frac": round((sum(fwd_f) + sum(bwd_f)) / (t_s / steps) / FP32_MFMA_PEAK, 4),
            "predictive_samples_per_s": round(world * S / t_p, 3), "n_test": nt,
            "predictive_kernel_ms": round(k_ms, 3),
            "predictive_mfma_frac": round(fp / (k_ms * 1e-3) / FP32_MFMA_PEAK, 4)}
@@ -298,7 +299,7 @@ def main():
             "peak": FP32_MFMA_PEAK / 1e12, "unit": "TFLOP/s",
             "frac": round(fl_dom / (ms_dom * 1e-3) / FP32_MFMA_PEAK, 8),
             "traffic": pmc_traffic(dom),
-            "traffic_source": "profiles/r01b/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE "
+            "traffic_source": "profiles/r02/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE "
                               "passes of this bench; bytes per launch incl. Infinity-Cache hits)",
             "avg_launch_us": round(ms_dom * 1e3, 3),
             "flops_per_launch": int(fl_dom),
