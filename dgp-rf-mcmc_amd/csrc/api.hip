@@ -371,6 +371,13 @@ int dgprf_graph_create_sghmc(dgprf_graph_handle* out, const dgprf_plan_t* plan,
   if (step->full_bayes && plan->fresh_z) return DGPRF_E_ARG;
   hipStream_t cs;
   if (hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess) return DGPRF_E_HIP;
+  if (plan->a0_off >= 0) {  // library GEMM state (handle, tuned algorithm) before capture
+    const StepDev sd0 = make_step_dev(*plan, *chain, *batch, step->step_offset);
+    if (dgprf::launch_step_agemm(*plan, sd0, cs) != hipSuccess || hipStreamSynchronize(cs) != hipSuccess) {
+      (void)hipStreamDestroy(cs);
+      return DGPRF_E_HIP;
+    }
+  }
   hipError_t e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
   dgprf_step_t st = *step;
   st.grad_only = 0;

@@ -1,0 +1,147 @@
+// blas.hip — the one plain library GEMM of the path: A_1 = X Omega_1 of a wide first layer
+// (layers/rf_layers.py:29-45, the `tf.matmul(x, self.Omega)` of RBFLayer / ARCLayer when
+// d_1 > 32, e.g. the 784 MNIST pixels of config 4) on hipBLASLt, fp32 in / fp32 compute / fp32 out.
+//
+// Row-major A[n][R] = X[n][d] (row stride ldx) Omega[d][R] is, read column-major,
+// A^T (R x n, ld R) = Omega^T (R x d, ld R) X^T (d x n, ld ldx): a plain NN GEMM with no copies.
+// C chains (C > 1) run as one strided-batched GEMM (X and A strides per chain, Omega stride 0 when
+// shared).
+//
+// Algorithm choice per shape: hipBLASLt's heuristic candidates (no workspace) are timed once on the
+// first call outside stream capture and the fastest is cached, so every later call — eager or
+// captured into a hipGraph — runs the same kernel (bit-identical results).  A first call under
+// capture takes the heuristic's top candidate without timing.  No candidate: the caller launches
+// its own k_step_agemm instead.
+#include <hipblaslt/hipblaslt.h>
+
+#include <map>
+#include <mutex>
+#include <tuple>
+#include <vector>
+
+#include "dgprf_internal.h"
+
+namespace {
+
+struct GemmKey {
+  int dev;
+  int64_t n, R, d, ldx, batch, sx, so, sa;
+  bool operator<(const GemmKey& o) const {
+    return std::tie(dev, n, R, d, ldx, batch, sx, so, sa) <
+           std::tie(o.dev, o.n, o.R, o.d, o.ldx, o.batch, o.sx, o.so, o.sa);
+  }
+};
+
+struct GemmPlan {
+  hipblasLtMatmulDesc_t op = nullptr;
+  hipblasLtMatrixLayout_t la = nullptr, lb = nullptr, lc = nullptr;
+  hipblasLtMatmulAlgo_t algo;
+  bool ok = false;
+};
+
+std::mutex g_mu;
+std::map<int, hipblasLtHandle_t> g_handles;
+std::map<GemmKey, GemmPlan> g_plans;
+
+bool layout(hipblasLtMatrixLayout_t* l, int64_t rows, int64_t cols, int64_t ld, int64_t batch,
+            int64_t stride) {
+  if (hipblasLtMatrixLayoutCreate(l, HIP_R_32F, rows, cols, ld) != HIPBLAS_STATUS_SUCCESS)
+    return false;
+  if (batch > 1) {
+    int32_t b = (int32_t)batch;
+    if (hipblasLtMatrixLayoutSetAttribute(*l, HIPBLASLT_MATRIX_LAYOUT_BATCH_COUNT, &b, sizeof(b)) !=
+            HIPBLAS_STATUS_SUCCESS ||
+        hipblasLtMatrixLayoutSetAttribute(*l, HIPBLASLT_MATRIX_LAYOUT_STRIDED_BATCH_OFFSET, &stride,
+                                          sizeof(stride)) != HIPBLAS_STATUS_SUCCESS)
+      return false;
+  }
+  return true;
+}
+
+}  // namespace
+
+namespace dgprf {
+
+bool blas_agemm(const float* X, int64_t n, int ldx, int d, const float* om, int R, float* aout,
+                int batch, int64_t sx, int64_t so, int64_t sa, hipStream_t s) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cap) != hipSuccess) return false;
+  const bool capturing = cap != hipStreamCaptureStatusNone;
+  std::lock_guard<std::mutex> lock(g_mu);
+  auto hit = g_handles.find(dev);
+  if (hit == g_handles.end()) {
+    if (capturing) return false;  // the handle is created outside capture
+    hipblasLtHandle_t h;
+    if (hipblasLtCreate(&h) != HIPBLAS_STATUS_SUCCESS) return false;
+    hit = g_handles.emplace(dev, h).first;
+  }
+  hipblasLtHandle_t h = hit->second;
+  const GemmKey key{dev, n, R, d, ldx, batch, sx, so, sa};
+  auto it = g_plans.find(key);
+  const float alpha = 1.f, beta = 0.f;
+  if (it == g_plans.end()) {
+    GemmPlan p;
+    const bool built =
+        hipblasLtMatmulDescCreate(&p.op, HIPBLAS_COMPUTE_32F, HIP_R_32F) == HIPBLAS_STATUS_SUCCESS &&
+        layout(&p.la, R, d, R, batch, so) && layout(&p.lb, d, n, ldx, batch, sx) &&
+        layout(&p.lc, R, n, R, batch, sa);
+    std::vector<hipblasLtMatmulHeuristicResult_t> res(16);
+    int nres = 0;
+    hipblasLtMatmulPreference_t pref = nullptr;
+    if (built && hipblasLtMatmulPreferenceCreate(&pref) == HIPBLAS_STATUS_SUCCESS) {
+      uint64_t ws = 0;
+      hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &ws,
+                                            sizeof(ws));
+      if (hipblasLtMatmulAlgoGetHeuristic(h, p.op, p.la, p.lb, p.lc, p.lc, pref, (int)res.size(),
+                                          res.data(), &nres) != HIPBLAS_STATUS_SUCCESS)
+        nres = 0;
+      hipblasLtMatmulPreferenceDestroy(pref);
+    }
+    int best = -1;
+    if (nres > 0 && capturing) {
+      best = 0;
+    } else if (nres > 0) {
+      // time each candidate (3 warm + 10 timed runs on this stream; the output is rewritten by
+      // the real call below)
+      hipEvent_t e0, e1;
+      hipEventCreate(&e0);
+      hipEventCreate(&e1);
+      float best_ms = 0.f;
+      for (int i = 0; i < nres; ++i) {
+        if (res[i].state != HIPBLAS_STATUS_SUCCESS || res[i].workspaceSize != 0) continue;
+        bool ok = true;
+        for (int r = 0; r < 3 && ok; ++r)
+          ok = hipblasLtMatmul(h, p.op, &alpha, om, p.la, X, p.lb, &beta, aout, p.lc, aout, p.lc,
+                               &res[i].algo, nullptr, 0, s) == HIPBLAS_STATUS_SUCCESS;
+        if (!ok) continue;
+        hipEventRecord(e0, s);
+        for (int r = 0; r < 10; ++r)
+          hipblasLtMatmul(h, p.op, &alpha, om, p.la, X, p.lb, &beta, aout, p.lc, aout, p.lc,
+                          &res[i].algo, nullptr, 0, s);
+        hipEventRecord(e1, s);
+        hipEventSynchronize(e1);
+        float ms = 0.f;
+        hipEventElapsedTime(&ms, e0, e1);
+        if (best < 0 || ms < best_ms) {
+          best = i;
+          best_ms = ms;
+        }
+      }
+      hipEventDestroy(e0);
+      hipEventDestroy(e1);
+    }
+    if (best >= 0) {
+      p.algo = res[best].algo;
+      p.ok = true;
+    }
+    it = g_plans.emplace(key, p).first;
+  }
+  const GemmPlan& p = it->second;
+  if (!p.ok) return false;
+  return hipblasLtMatmul(h, p.op, &alpha, om, p.la, X, p.lb, &beta, aout, p.lc, aout, p.lc,
+                         &p.algo, nullptr, 0, s) == HIPBLAS_STATUS_SUCCESS;
+}
+
+}  // namespace dgprf

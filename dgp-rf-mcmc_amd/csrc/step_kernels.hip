@@ -2018,6 +2018,32 @@ extern "C" int dgprf_debug_clear_stamps(void) {
 
 namespace dgprf {
 
+// A_1 = X Omega_1 of the step's gathered rows into the workspace (plan.a0_off): hipBLASLt, or
+// k_step_agemm when the library has no candidate for the shape (or its handle would have to be
+// created under stream capture).
+hipError_t launch_step_agemm(const dgprf_plan_t& pl, const StepDev& sd, hipStream_t s) {
+  int lds_floats = 0;
+  const LayerK a = make_layer_k(pl, sd, 0, lds_floats);
+  if (!a.a0) return hipSuccess;
+  if (blas_agemm(a.xrows, pl.batch, pl.d_in, pl.d[0], a.om, pl.n_rf[0], sd.ws + pl.a0_off,
+                 pl.n_chains, a.xrow_cs, a.om_cs, pl.ws_chain, s))
+    return hipSuccess;
+  AgemmK g;
+  g.xrows = a.xrows;
+  g.om = a.om;
+  g.aout = sd.ws + pl.a0_off;
+  g.xrow_cs = a.xrow_cs;
+  g.om_cs = a.om_cs;
+  g.ws_cs = pl.ws_chain;
+  g.B = pl.batch;
+  g.d = pl.d[0];
+  g.R = pl.n_rf[0];
+  g.d_in = pl.d_in;
+  dim3 ggrid((unsigned)((g.R + 63) / 64), (unsigned)((g.B + 31) / 32), pl.n_chains);
+  hipLaunchKernelGGL(k_step_agemm, ggrid, dim3(256), 0, s, g);
+  return hipGetLastError();
+}
+
 hipError_t launch_step_fwd(const dgprf_plan_t& pl, const StepDev& sd, int layer, hipStream_t s,
                            const UpdateDev* ud, bool pend) {
   pend = pend && ud && layer == 0 && pl.fused_update == 1 && pl.n_gp[0] <= 16 && pl.d[0] <= 32;
@@ -2035,20 +2061,9 @@ hipError_t launch_step_fwd(const dgprf_plan_t& pl, const StepDev& sd, int layer,
     a.smap = 1;
     a.main_blocks = 8 * ((a.ns + 7) / 8) * a.n_rt;
   }
-  if (a.a0) {  // wide first layer: A_1 = X Omega_1 first (k_step_agemm)
-    AgemmK g;
-    g.xrows = a.xrows;
-    g.om = a.om;
-    g.aout = sd.ws + pl.a0_off;
-    g.xrow_cs = a.xrow_cs;
-    g.om_cs = a.om_cs;
-    g.ws_cs = pl.ws_chain;
-    g.B = pl.batch;
-    g.d = pl.d[0];
-    g.R = pl.n_rf[0];
-    g.d_in = pl.d_in;
-    dim3 ggrid((unsigned)((g.R + 63) / 64), (unsigned)((g.B + 31) / 32), pl.n_chains);
-    hipLaunchKernelGGL(k_step_agemm, ggrid, dim3(256), 0, s, g);
+  if (a.a0) {  // wide first layer: A_1 = X Omega_1 first
+    const hipError_t e = launch_step_agemm(pl, sd, s);
+    if (e != hipSuccess) return e;
   }
   dim3 grid(a.main_blocks, 1, pl.n_chains);
   k_step_fwd_launch(pl.d[layer], pl.n_gp[layer], pl.kind[layer] == DGPRF_RBF, pend, w8, grid,
@@ -2213,6 +2228,7 @@ hipError_t launch_step_update(const dgprf_plan_t& pl, const StepDev& sd, const U
 hipError_t launch_agemm(const float* X, int64_t n, int ld, int d, const float* om, int R,
                         float* aout, hipStream_t s) {
   if (n <= 0) return hipSuccess;
+  if (n <= INT32_MAX && blas_agemm(X, n, ld, d, om, R, aout, 1, 0, 0, 0, s)) return hipSuccess;
   if (n > INT32_MAX || (int64_t)n * ld >= ((int64_t)1 << 29) || (int64_t)d * R >= ((int64_t)1 << 29))
     return hipErrorInvalidValue;  // 32-bit buffer offsets
   AgemmK g;
