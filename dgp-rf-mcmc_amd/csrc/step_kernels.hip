@@ -1277,8 +1277,8 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2 ld2(const float* p) { return *reinterpret_cast<const f2*>(p); }
 __device__ __forceinline__ void st2(float* p, f2 v) { *reinterpret_cast<f2*>(p) = v; }
 
-// One wave per workgroup, two parameters per lane: the gW partial sums (16 row tiles x 8 bytes
-// per lane) are spread over >= 256 workgroups instead of concentrated on a few CUs; row tiles
+// One wave per workgroup, four parameters per lane: the gW partial sums (16 row tiles x 16 bytes
+// per lane) are spread over many workgroups instead of concentrated on a few CUs; row tiles
 // past n_row_tiles and lanes past w_total lie outside the buffer descriptors (zero, no memory
 // traffic), so every load is issued before the first branch.  Specialised on the rarely-used
 // paths: GIN (gradient supplied), GONLY (gradient only), XI (injected noise), CYC (cyclical).
@@ -1576,23 +1576,25 @@ __global__ __launch_bounds__(UPD_THREADS) void k_step_update(const UpdK a) {
                  a.yb + (int64_t)chain * a.ws_cs, chain, t + 1, b);
     return;
   }
-  const int e0 = 2 * (bx * UPD_THREADS + (int)threadIdx.x);
+  // four packed parameters per lane (one counter quad of Philox normals, 16-byte loads); layer
+  // offsets are multiples of 4, so a quad never straddles two layers
+  const int e0 = 4 * (bx * UPD_THREADS + (int)threadIdx.x);
   const uint32_t off = (uint32_t)e0 * 4u;
   const int64_t cw = (int64_t)chain * a.w_total;
   const rsrc_t rth = make_rsrc(a.theta + cw, a.w_total);
-  const f2 th = bload2(rth, off);
-  f2 m = {0.f, 0.f}, gr;
-  if (!GONLY) m = bload2(make_rsrc(a.mom + cw, a.w_total), off);
+  const f4 th = bload4(rth, off);
+  f4 m = f4zero(), gr;
+  if (!GONLY) m = bload4(make_rsrc(a.mom + cw, a.w_total), off);
   if (GIN) {
-    gr = bload2(make_rsrc(a.grad_in + cw, a.w_total), off);
+    gr = bload4(make_rsrc(a.grad_in + cw, a.w_total), off);
   } else {
     // sum the row-tile gW partials in a fixed order: groups of 16 independent loads
     const rsrc_t rs = make_rsrc(a.gwp + (int64_t)chain * a.ws_cs, (int64_t)a.n_rt * a.w_total);
-    f2 sacc = {0.f, 0.f};
+    f4 sacc = f4zero();
     for (int rt0 = 0; rt0 < a.n_rt_pad; rt0 += 16) {
-      f2 v[16];
+      f4 v[16];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) v[j] = bload2(rs, (uint32_t)(((rt0 + j) * a.w_total + e0) * 4));
+      for (int j = 0; j < 16; ++j) v[j] = bload4(rs, (uint32_t)(((rt0 + j) * a.w_total + e0) * 4));
 #pragma unroll
       for (int j = 0; j < 16; ++j) sacc += v[j];
     }
@@ -1602,13 +1604,21 @@ __global__ __launch_bounds__(UPD_THREADS) void k_step_update(const UpdK a) {
 #pragma unroll
   for (int l = 1; l < DGPRF_MAX_LAYERS; ++l)
     if (l < a.n_layers && e0 >= a.lo[l]) layer = l;
-  const bool live = e0 < a.hi[layer];  // layer padding between align4 offsets stays untouched
+  // layer padding between align4 offsets stays untouched: live elements of the quad
+  const int nlive = min(max(a.hi[layer] - e0, 0), 4);
+  auto store = [&](float* p, f4 v) {
+    if (nlive == 4) {
+      st4(p, v);
+    } else {
+      for (int k = 0; k < nlive; ++k) p[k] = v[k];
+    }
+  };
   const UpdateDev& ud = a.ud;
   const float N = ud.data_size;
   // dU/dW = W/N (prior N(0,1), models/dgp.py:129-136,171) + Phi^T dF (likelihood)
   if (!GIN) gr = th / N + gr;
   if (GONLY) {
-    if (live) st2(a.grad_out + (int64_t)chain * a.grad_cs + e0, gr);
+    store(a.grad_out + (int64_t)chain * a.grad_cs + e0, gr);
     return;
   }
   const float M = a.mass[chain * a.n_layers + layer];
@@ -1621,30 +1631,18 @@ __global__ __launch_bounds__(UPD_THREADS) void k_step_update(const UpdK a) {
   const float h = sqrtf(lr / N);
   const float beta = ud.beta;
   const uint32_t quad = (uint32_t)(e0 >> 2);
-  const int half = (e0 >> 1) & 1;
   if (resample) {  // models/dgp.py:209-210 (ignores M, Appendix A.1)
-    if (XI && ud.xi_resample) {
-      m = ld2(ud.xi_resample + cw + e0);
-    } else {
-      float z0, z1;
-      philox_normal2(a.seed, (uint64_t)t, DGPRF_RNG_RESAMPLE, chain, quad, half, &z0, &z1);
-      m = f2{z0, z1};
-    }
+    if (XI && ud.xi_resample)
+      m = ld4(ud.xi_resample + cw + e0);
+    else
+      m = philox_normal4(a.seed, (uint64_t)t, DGPRF_RNG_RESAMPLE, (uint32_t)chain, quad);
   }
-  f2 mn = beta * m - (h * N) * gr;
-  f2 eps;
-  if (XI && ud.xi) {
-    eps = ld2(ud.xi + cw + e0);
-  } else {
-    float z0, z1;
-    philox_normal2(a.seed, (uint64_t)t, DGPRF_RNG_NOISE, chain, quad, half, &z0, &z1);
-    eps = f2{z0, z1};
-  }
+  f4 mn = beta * m - (h * N) * gr;
+  const f4 eps = (XI && ud.xi) ? ld4(ud.xi + cw + e0)
+                               : philox_normal4(a.seed, (uint64_t)t, DGPRF_RNG_NOISE, (uint32_t)chain, quad);
   mn = mn + sqrtf(2.0f * (1.0f - beta) * T * M) * eps;
-  if (live) {
-    st2(a.mom + cw + e0, mn);
-    st2(a.theta + cw + e0, th + (h * (1.0f / M)) * mn);
-  }
+  store(a.mom + cw + e0, mn);
+  store(a.theta + cw + e0, th + (h * (1.0f / M)) * mn);
 #ifdef DGPRF_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
@@ -2147,8 +2145,8 @@ hipError_t launch_step_update(const dgprf_plan_t& pl, const StepDev& sd, const U
   a.bd = sd.bd;
   a.xb = sd.ws ? sd.ws + pl.xb_off : nullptr;
   a.yb = sd.ws ? sd.ws + pl.yb_off : nullptr;
-  const int64_t pairs = pl.w_total / 2;
-  a.upd_blocks = (int)((pairs + UPD_THREADS - 1) / UPD_THREADS);
+  const int64_t quads = pl.w_total / 4;
+  a.upd_blocks = (int)((quads + UPD_THREADS - 1) / UPD_THREADS);
   const bool gin = grad_in != nullptr, gonly = ud.grad_only != 0;
   const bool fb = sd.full_bayes && !gin;
   // full_bayesian=True: hyper workgroups first (per layer ceil(d R / HYP_EPB) for the Omega
