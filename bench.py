@@ -117,6 +117,24 @@ def pmc_traffic(prefix):
     return round(sum(v["traffic"] * v["dispatches"] for v in sel) / n) if n else None
 
 
+def rocprof_avg_us(prefix):
+    """Dispatch-weighted average duration (us) of the kernels named `prefix...` in the committed
+    rocprofv3 --kernel-trace --stats summary of this bench (profiles/r02/kernel_stats_bench.csv);
+    None if absent.  Traced durations include each dispatch's own launch overhead."""
+    import csv
+    path = os.path.join(ROOT, "profiles", "r02", "kernel_stats_bench.csv")
+    if not os.path.exists(path):
+        return None
+    n = tot = 0.0
+    with open(path) as fh:
+        for r in csv.DictReader(fh):
+            name = r["Name"].replace("void ", "").replace("(anonymous namespace)::", "")
+            if name.startswith(prefix + "<") or name.startswith(prefix + "("):
+                n += float(r["Calls"])
+                tot += float(r["TotalDurationNs"])
+    return round(tot / n / 1e3, 3) if n else None
+
+
 def bench_config(cfg, dev, rank, world, barrier_sync, max_over_ranks, steps):
     """Steps/s and predictive samples/s of BASELINE config 3, 4 or 5 (dgprf.data.CONFIGS): the full
     model shape on synthetic data of the config's size, one chain per GPU, graph-replayed steps."""
@@ -304,6 +322,11 @@ def main():
             "avg_launch_us": round(ms_dom * 1e3, 3),
             "flops_per_launch": int(fl_dom),
             "method": "hipEvent pair around the kernel minus an empty pair (dgprf_profile_step)",
+            "rocprof_avg_launch_us": rocprof_avg_us(dom),
+            "rocprof_note": "profiles/r02/kernel_stats_bench.csv (rocprofv3 --kernel-trace of this bench); "
+                            "traced durations include each dispatch's launch overhead, the event "
+                            "difference is the in-kernel span; step_us_events / launches per step "
+                            "is the boundary-inclusive share",
             "step_us_events": round(step_ms_dev * 1e3, 3),
             "empty_pair_us": round(prof["empty"] * 1e3, 3),
             "step_kernel_us": {"fwd": [round(x * 1e3, 3) for x in att_fwd],
@@ -320,6 +343,7 @@ def main():
                  "traffic": pmc_traffic("k_forward_tiles"),
                  "algorithmic_bytes": int(4 * CFG["N_test"] * (CFG["D"] + 1 + 3 * 2)),
                  "avg_launch_us": round(pred_kernel_ms * 1e3, 2),
+                 "rocprof_avg_launch_us": rocprof_avg_us("k_forward_tiles"),
                  "flops_per_launch": int(fp)}
 
     # ---------------- many chains per GPU (aggregate chain-steps/s; extra, not `value`)
