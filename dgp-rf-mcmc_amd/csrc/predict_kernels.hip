@@ -967,12 +967,17 @@ ForwardCfg forward_cfg(const dgprf_plan_t& pl, int64_t n) {
   // rows it leaves most SIMDs idle, and the row kernel with 16 waves per tile (each a sixteenth
   // of every layer's features, F partials summed in LDS) covers the chip instead
   constexpr int64_t FWD_TILE_MIN_ROWS = 16384;
-  const bool few = n < FWD_TILE_MIN_ROWS && small && !c.wide0;
+  const bool few = n < FWD_TILE_MIN_ROWS;
+  // layers with g > 16 run the tile kernel at 2 waves per SIMD (its 2-4 output tiles per wave do
+  // not fit 4): the 4-wave row kernel is faster at every measured size (config 4: 10k / 20k / 40k
+  // test rows 1,072 / 1,923 / 3,716 us vs 1,167 / 2,321 / 4,026 us on the tile kernel)
+  bool wide_g = false;
+  for (int l = 0; l < pl.n_layers; ++l) wide_g = wide_g || pl.n_gp[l] > 16;
   switch (pl.fwd_path) {
     case DGPRF_FWD_ROWS: c.tiles = false; c.rows_waves = 4; break;
     case DGPRF_FWD_ROWS16: c.tiles = false; c.rows_waves = small ? 16 : 4; break;
     case DGPRF_FWD_TILE: c.tiles = tile_ok; c.rows_waves = 4; break;
-    default: c.tiles = tile_ok && !few; c.rows_waves = few ? 16 : 4; break;
+    default: c.tiles = tile_ok && !few && !wide_g; c.rows_waves = few && small ? 16 : 4; break;
   }
   // chunks are whole 64-row tile-kernel workgroups: every wave of the last workgroup reads its 16
   // A_1 rows (rows past n included, their outputs discarded), so the scratch covers align64 rows

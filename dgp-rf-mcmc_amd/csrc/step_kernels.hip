@@ -1916,10 +1916,10 @@ void set_update_range(LayerK& a, const dgprf_plan_t& pl, int layer, int t_off, i
   }
 
 // forward: KS x NOT x RBF x G1 (x PEND for the narrow layers the fused update covers: NOT == 1) x
-// waves per workgroup (8 for slices of >= 2 chunks per wave: two waves per SIMD hide each other's
-// MFMA / load latency; 4 otherwise and with PEND)
+// waves per workgroup (8 / 16 for slices of >= 2 chunks per wave: two / four waves per SIMD hide
+// each other's MFMA / load latency; 4 otherwise and with PEND)
 template <int KS, int NOT, bool G1>
-void k_step_fwd_launch3(bool rbf, bool pend, bool w8, dim3 grid, size_t lds, hipStream_t s,
+void k_step_fwd_launch3(bool rbf, bool pend, int nw, dim3 grid, size_t lds, hipStream_t s,
                         const LayerK& a) {
 #define DGPRF_FWD(R_, P_, W_)                                                                  \
   do {                                                                                        \
@@ -1929,7 +1929,10 @@ void k_step_fwd_launch3(bool rbf, bool pend, bool w8, dim3 grid, size_t lds, hip
   if (pend && NOT == 1) {
     if (rbf) DGPRF_FWD(true, NOT == 1, 4);
     else DGPRF_FWD(false, NOT == 1, 4);
-  } else if (w8) {
+  } else if (nw == 16) {
+    if (rbf) DGPRF_FWD(true, false, 16);
+    else DGPRF_FWD(false, false, 16);
+  } else if (nw == 8) {
     if (rbf) DGPRF_FWD(true, false, 8);
     else DGPRF_FWD(false, false, 8);
   } else {
@@ -1939,22 +1942,22 @@ void k_step_fwd_launch3(bool rbf, bool pend, bool w8, dim3 grid, size_t lds, hip
 #undef DGPRF_FWD
 }
 template <int KS>
-void k_step_fwd_launch2(int g, bool rbf, bool pend, bool w8, dim3 grid, size_t lds, hipStream_t s,
+void k_step_fwd_launch2(int g, bool rbf, bool pend, int nw, dim3 grid, size_t lds, hipStream_t s,
                         const LayerK& a) {
   const int NOT = (g + 15) >> 4;
-  if (g == 1) k_step_fwd_launch3<KS, 1, true>(rbf, pend, w8, grid, lds, s, a);
-  else if (NOT == 1) k_step_fwd_launch3<KS, 1, false>(rbf, pend, w8, grid, lds, s, a);
-  else if (NOT == 2) k_step_fwd_launch3<KS, 2, false>(rbf, false, w8, grid, lds, s, a);
-  else if (NOT == 3) k_step_fwd_launch3<KS, 3, false>(rbf, false, w8, grid, lds, s, a);
-  else k_step_fwd_launch3<KS, 4, false>(rbf, false, w8, grid, lds, s, a);
+  if (g == 1) k_step_fwd_launch3<KS, 1, true>(rbf, pend, nw, grid, lds, s, a);
+  else if (NOT == 1) k_step_fwd_launch3<KS, 1, false>(rbf, pend, nw, grid, lds, s, a);
+  else if (NOT == 2) k_step_fwd_launch3<KS, 2, false>(rbf, false, nw, grid, lds, s, a);
+  else if (NOT == 3) k_step_fwd_launch3<KS, 3, false>(rbf, false, nw, grid, lds, s, a);
+  else k_step_fwd_launch3<KS, 4, false>(rbf, false, nw, grid, lds, s, a);
 }
-void k_step_fwd_launch(int d, int g, bool rbf, bool pend, bool w8, dim3 grid, size_t lds,
+void k_step_fwd_launch(int d, int g, bool rbf, bool pend, int nw, dim3 grid, size_t lds,
                        hipStream_t s, const LayerK& a) {
-  if (d <= 4) k_step_fwd_launch2<1>(g, rbf, pend, w8, grid, lds, s, a);
-  else if (d <= 8) k_step_fwd_launch2<2>(g, rbf, pend, w8, grid, lds, s, a);
-  else if (d <= 16) k_step_fwd_launch2<4>(g, rbf, pend, w8, grid, lds, s, a);
-  else if (d <= 32) k_step_fwd_launch2<8>(g, rbf, pend, w8, grid, lds, s, a);
-  else k_step_fwd_launch2<0>(g, rbf, false, w8, grid, lds, s, a);
+  if (d <= 4) k_step_fwd_launch2<1>(g, rbf, pend, nw, grid, lds, s, a);
+  else if (d <= 8) k_step_fwd_launch2<2>(g, rbf, pend, nw, grid, lds, s, a);
+  else if (d <= 16) k_step_fwd_launch2<4>(g, rbf, pend, nw, grid, lds, s, a);
+  else if (d <= 32) k_step_fwd_launch2<8>(g, rbf, pend, nw, grid, lds, s, a);
+  else k_step_fwd_launch2<0>(g, rbf, false, nw, grid, lds, s, a);
 }
 
 // backward: KS x NOT x RBF x G1 x FB x waves per workgroup (8: W-only with whole-slice staging)
@@ -2048,8 +2051,11 @@ hipError_t launch_step_fwd(const dgprf_plan_t& pl, const StepDev& sd, int layer,
   // 8 waves per workgroup when every wave still gets >= 2 chunks and no pending update is applied
   // (config 3, cpw = 2: one chunk per wave measured slower, 37.6 vs 35.9 us/step)
   const bool w8 = !pend && pl.cpw[layer] >= 4 && pl.cpw[layer] % 2 == 0;
+  // 16 waves (four per SIMD) when every wave still gets >= 2 chunks (config 5, cpw = 8:
+  // 104.4 -> 102.4 us/step; with one chunk per wave, config 4, no gain)
+  const int nwf = (w8 && pl.cpw[layer] % 8 == 0) ? 16 : (w8 ? 8 : 4);
   int lds_floats = 0;
-  LayerK a = make_layer_k(pl, sd, layer, lds_floats, false, w8 ? 8 : 4);
+  LayerK a = make_layer_k(pl, sd, layer, lds_floats, false, nwf);
   if (pend) {  // the previous step's W_1 update, applied by this forward (its step offset - 1)
     fill_fused(a, pl, sd, *ud);
     a.pend = 1;
@@ -2064,7 +2070,7 @@ hipError_t launch_step_fwd(const dgprf_plan_t& pl, const StepDev& sd, int layer,
     if (e != hipSuccess) return e;
   }
   dim3 grid(a.main_blocks, 1, pl.n_chains);
-  k_step_fwd_launch(pl.d[layer], pl.n_gp[layer], pl.kind[layer] == DGPRF_RBF, pend, w8, grid,
+  k_step_fwd_launch(pl.d[layer], pl.n_gp[layer], pl.kind[layer] == DGPRF_RBF, pend, nwf, grid,
                     (size_t)lds_floats * sizeof(float), s, a);
   return hipGetLastError();
 }
