@@ -267,13 +267,13 @@ __device__ __forceinline__ void elem_issue(const LayerK& a, int chain, int row0,
 }
 // sum + store: xs[dst] or dfs[dst] (and ysh[dst]); non-owning lanes write a scratch slot
 __device__ __forceinline__ void elem_store(const Elem& e, float* xs, float* dfs, float* ysh,
-                                          float* scratch) {
+                                          float* scratch, int np) {
   float acc = e.v[0];
 #pragma unroll
   for (int sl = 1; sl < NSM; ++sl) acc += e.v[sl];
   const float val = e.isx ? acc + e.xd : acc;  // exactly one of the two is non-zero-sourced
   float* dv = e.dst < 0 ? scratch : (e.isx ? xs + e.dst : dfs + e.dst);
-  float* dy = (e.dst < 0 || e.isx) ? scratch + 256 : ysh + e.dst;
+  float* dy = (e.dst < 0 || e.isx) ? scratch + np : ysh + e.dst;
   *dv = val;
   *dy = e.y;
 }
@@ -284,13 +284,14 @@ __device__ __forceinline__ void elem_prologue(const LayerK& a, int chain, int ro
                                              float* scratch) {
   const int total = TR * round4(a.d) + nd_tile;
   const int t = threadIdx.x;
-  if (t >= 256) return;  // 8-wave workgroups: waves 0-3 own the elements (wave-uniform)
+  const int np = min((int)blockDim.x, 512);  // owning threads: elements t and t + np
+  if (t >= np) return;  // 16-wave workgroups: waves 0-7 own the elements (wave-uniform)
   const int wave0 = __builtin_amdgcn_readfirstlane(t & ~63);
   Elem e0, e1;
   if (wave0 < total) elem_issue(a, chain, row0, t, nd_tile, dfst, e0);
-  if (256 + wave0 < total) elem_issue(a, chain, row0, t + 256, nd_tile, dfst, e1);
-  if (wave0 < total) elem_store(e0, xs, dfs, ysh, scratch + t);
-  if (256 + wave0 < total) elem_store(e1, xs, dfs, ysh, scratch + t);
+  if (np + wave0 < total) elem_issue(a, chain, row0, t + np, nd_tile, dfst, e1);
+  if (wave0 < total) elem_store(e0, xs, dfs, ysh, scratch + t, np);
+  if (np + wave0 < total) elem_store(e1, xs, dfs, ysh, scratch + t, np);
 }
 
 // Omega fragments: omk[ks] = Omega[4ks+lq][f0+lr] (zero outside the layer), KS k-steps.
@@ -1811,8 +1812,13 @@ LayerK make_layer_k(const dgprf_plan_t& pl, const StepDev& sd, int l, int& lds_f
   a.ws = sd.ws;
   a.fprev_off = l > 0 ? (int)pl.fp_off[l - 1] : 0;
   a.dsrc_off = a.last ? (int)pl.fp_off[l] : (l + 1 < pl.n_layers ? (int)pl.dxp_off[l + 1] : 0);
-  a.fast = sd.ws != nullptr && TR * (dpad + a.g) <= 512 && a.g <= 16 && a.gp <= 16 &&
-           a.R % 4 == 0 && pl.ws_chain < (1 << 29);
+  // element-owner prologue: up to two elements per thread of the first min(threads, 512); the
+  // 4-wave backward also stages its 64-feature W / Omega block by float4 (g, g_{l-1} <= 16), the
+  // whole-slice (8-wave) backward and the forward stage nothing there
+  const int pro_cap = 2 * min(64 * nwb, 512);
+  const bool blk4 = bwd && nwb < 8;
+  a.fast = sd.ws != nullptr && TR * (dpad + (bwd ? a.g : 0)) <= pro_cap &&
+           (!blk4 || (a.g <= 16 && a.gp <= 16)) && a.R % 4 == 0 && pl.ws_chain < (1 << 29);
   a.xmag = div_magic(dpad);
   a.dmag = div_magic(a.g);
   a.n_rt = pl.n_row_tiles;
