@@ -255,14 +255,16 @@ def main():
                steps_per_graph=args.steps_per_graph, perm_seed=rank_seed(0, rank))
 
     # ---------------- SGHMC steps (graph-replayed, on-device minibatching)
-    # Every hipGraph the timed call replays is captured, instantiated and launched once here
-    # (untimed), so the timed region is replays only; then the W warm-up steps.
+    # Every hipGraph the timed call replays is captured and instantiated here, the W warm-up steps
+    # run, and then each timed graph is launched once (untimed) right before the clock: the timed
+    # region is replays only, and its first replay does not follow a different graph (measured
+    # +2.5 us/step on the driver's 20-step run when it did, scripts/diag/driver_shape.py).
     timed_plan = model.sgmcmc_graphs(X, Y, N_, args.steps, **run)
     timed_graphs = [{"steps_per_graph": gph.steps, "replays": reps} for gph, reps in timed_plan]
-    for gph, _ in timed_plan:
-        gph.launch()
     if args.warmup > 0:
         model.run_sgmcmc(X, Y, N_, args.warmup, **run)
+    for gph, _ in timed_plan:
+        gph.launch()
     barrier_sync()
     es0, es1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
