@@ -173,7 +173,7 @@ int dgprf_plan_init(dgprf_plan_t* pl) {
   if (L < 1 || L > DGPRF_MAX_LAYERS) return DGPRF_E_SHAPE;
   if (pl->d_in < 1 || pl->d_out < 1 || pl->batch < 1 || pl->n_chains < 1) return DGPRF_E_SHAPE;
   if (pl->likelihood != DGPRF_LIK_GAUSSIAN && pl->likelihood != DGPRF_LIK_SOFTMAX) return DGPRF_E_ARG;
-  if (pl->fwd_path < DGPRF_FWD_AUTO || pl->fwd_path > DGPRF_FWD_ROWS16 || pl->agemm_chunk_rows < 0 ||
+  if (pl->fwd_path < DGPRF_FWD_AUTO || pl->fwd_path > DGPRF_FWD_ROWS8 || pl->agemm_chunk_rows < 0 ||
       (pl->fuse_update != 0 && pl->fuse_update != 1) || pl->fresh_z < 0 ||
       (pl->fresh_z >> L) != 0)
     return DGPRF_E_ARG;

@@ -19,6 +19,9 @@
 namespace {
 
 constexpr int NW = DGPRF_WAVES;
+#ifndef DGPRF_ROWS16_WPE
+#define DGPRF_ROWS16_WPE 8
+#endif
 constexpr int TR = DGPRF_TILE_ROWS;
 constexpr float LOG_2PI = 1.8378770664093453f;
 
@@ -38,7 +41,9 @@ __host__ __device__ inline FwdLds fwd_lds(const dgprf_plan_t& pl, int nwr = NW) 
   L.xst = round4(dmax) + 1;
   L.ftst = round4(gmax) + 1;
   L.red_off = round4(TR * L.xst);
-  L.ft_off = L.red_off + nwr * TR * 64;
+  // per-wave F partials [16 rows][16 x output tiles]: sized for the model's widest layer, so the
+  // 8- and 16-wave kernels fit two workgroups per CU
+  L.ft_off = L.red_off + nwr * TR * (((gmax + 15) >> 4) << 4);
   L.total = L.ft_off + round4(TR * L.ftst);
   return L;
 }
@@ -53,18 +58,23 @@ struct FOut {
 // MFMA chains are independent; cos and sin products accumulate in separate chains.  G1 (g == 1):
 // the W^T Phi^T product is a per-lane dot product (VALU) reduced over the 4 lane groups, instead of
 // a 16x16 MFMA tile that would be 15/16 padding.
-template <bool SMALLD, int NOT, bool RBF, bool G1, int NWR>
+// NKS: k-steps of A = Omega^T x when SMALLD (2, 4 or 8 >= ceil(d / 4), picked per layer by the
+// caller): compile-time, so the Omega loads and A-tile MFMAs carry no per-k-step branch (a runtime
+// count put every load and MFMA behind its own branch and wait: ≈2 us per chunk group on config 3);
+// k-steps past d load zeros (out-of-range buffer offsets) against zero x fragments.
+template <bool SMALLD, int NOT, bool RBF, bool G1, int NWR, int NKS>
 __device__ __forceinline__ void layer_partial(const float* __restrict__ om,
                                               const float* __restrict__ W, int R, int d, int g,
                                               float cl, const float* xs, int xst, float* red,
                                               int wave, int lr, int lq,
                                               const float* __restrict__ arow = nullptr) {
-  constexpr int CG = (NWR >= 16 || NOT > 1) ? 2 : 4;
-  float xf[8];
+  constexpr int CG = NWR >= 16 ? 1 : ((NWR >= 8 || NOT > 1) ? 2 : 4);
+  static_assert(NKS == 2 || NKS == 4 || NKS == 8, "k-step bucket");
+  float xf[NKS];
 #pragma unroll
-  for (int ks = 0; ks < 8; ++ks) xf[ks] = (SMALLD && 4 * ks < d) ? xs[lr * xst + 4 * ks + lq] : 0.f;
-  const int nks = (d + 3) >> 2;  // k-steps (SMALLD: <= 8)
-  float omk[CG][8], wf[CG][NOT][4][2];
+  for (int ks = 0; ks < NKS; ++ks) xf[ks] = (SMALLD && 4 * ks < d) ? xs[lr * xst + 4 * ks + lq] : 0.f;
+  const int nks = (d + 3) >> 2;  // k-steps of the !SMALLD loop
+  float omk[CG][NKS], wf[CG][NOT][4][2];
   // buffer loads: 32-bit offsets (one VGPR per address), masked lanes read 0 without traffic
   const rsrc_t ro = make_rsrc(om, SMALLD ? (int64_t)d * R : 0);
   const rsrc_t rw = make_rsrc(W, (int64_t)(RBF ? 2 : 1) * R * g);
@@ -72,10 +82,9 @@ __device__ __forceinline__ void layer_partial(const float* __restrict__ om,
     const int fa = f0 + lr;
     if (SMALLD) {
 #pragma unroll
-      for (int ks = 0; ks < 8; ++ks) {
+      for (int ks = 0; ks < NKS; ++ks) {
         const int k = 4 * ks + lq;
-        omk[j][ks] = ks < nks ? bload1(ro, fa < R && k < d ? (uint32_t)((k * R + fa) * 4) : DGPRF_OOB)
-                              : 0.f;
+        omk[j][ks] = bload1(ro, fa < R && k < d ? (uint32_t)((k * R + fa) * 4) : DGPRF_OOB);
       }
     }
 #pragma unroll
@@ -106,8 +115,7 @@ __device__ __forceinline__ void layer_partial(const float* __restrict__ om,
       f4 at = f4zero();
       if (SMALLD) {
 #pragma unroll
-        for (int ks = 0; ks < 8; ++ks)
-          if (ks < nks) at = mfma16(omk[j][ks], xf[ks], at);
+        for (int ks = 0; ks < NKS; ++ks) at = mfma16(omk[j][ks], xf[ks], at);
       } else if (arow) {  // precomputed A row (wide first layer): A[row lr][f0 + 4lq + r]
         at = *reinterpret_cast<const f4*>(arow + f0 + 4 * lq);
       } else {
@@ -166,8 +174,12 @@ __device__ __forceinline__ void layer_partial(const float* __restrict__ om,
 // One workgroup = one 16-row tile; its NWR waves split each layer's RF features (16-feature chunks
 // w, w + NWR, ...) and the per-wave F partials are summed in LDS in wave order.  NWR = 16 (4 waves
 // per SIMD) for test sets too small to fill the chip with the one-wave-per-tile tile kernel.
+// NWR = 8 / 16 are budgeted for two workgroups per CU (4 / 8 waves per SIMD): with one, a test set
+// of more tiles than CUs (config 3: 286) runs in two rounds.
 template <bool SMALLD, int NOTMAX, int NWR>
-__global__ __launch_bounds__(64 * NWR) void k_forward_rows(
+__global__ __launch_bounds__(64 * NWR)
+__attribute__((amdgpu_waves_per_eu(NWR == 16 ? DGPRF_ROWS16_WPE : (NWR == 8 ? 4 : 1))))
+void k_forward_rows(
     const dgprf_plan_t pl, const float* __restrict__ theta, const float* __restrict__ omega,
     const float* __restrict__ der, const float* __restrict__ X, const float* __restrict__ Y,
     const int y_cols, const int64_t n, const FOut fo, float* __restrict__ logp_out,
@@ -211,8 +223,15 @@ __global__ __launch_bounds__(64 * NWR) void k_forward_rows(
       const bool rbf = pl.kind[layer] == DGPRF_RBF;
       // runtime (layer) -> compile-time body: output tiles, kernel kind, g == 1 VALU path; layers
       // with d <= 32 take the register-fragment path even when another layer is wide
-#define DGPRF_LP(SD, NT, RB, G1_) \
-  layer_partial<SD, NT, RB, G1_, NWR>(om, W, R, d, g, cl, xs, LD.xst, red, wave, lr, lq, arow)
+#define DGPRF_LP(SD, NT, RB, G1_)                                                               \
+  do {                                                                                          \
+    if (!SD || d > 16)                                                                          \
+      layer_partial<SD, NT, RB, G1_, NWR, 8>(om, W, R, d, g, cl, xs, LD.xst, red, wave, lr, lq, arow); \
+    else if (d > 8)                                                                             \
+      layer_partial<SD, NT, RB, G1_, NWR, 4>(om, W, R, d, g, cl, xs, LD.xst, red, wave, lr, lq, arow); \
+    else                                                                                        \
+      layer_partial<SD, NT, RB, G1_, NWR, 2>(om, W, R, d, g, cl, xs, LD.xst, red, wave, lr, lq, arow); \
+  } while (0)
 #define DGPRF_LP_ALL(SD)                                                                        \
   do {                                                                                          \
     if (g == 1) {                                                                               \
@@ -976,6 +995,7 @@ ForwardCfg forward_cfg(const dgprf_plan_t& pl, int64_t n) {
   switch (pl.fwd_path) {
     case DGPRF_FWD_ROWS: c.tiles = false; c.rows_waves = 4; break;
     case DGPRF_FWD_ROWS16: c.tiles = false; c.rows_waves = small ? 16 : 4; break;
+    case DGPRF_FWD_ROWS8: c.tiles = false; c.rows_waves = small ? 8 : 4; break;
     case DGPRF_FWD_TILE: c.tiles = tile_ok; c.rows_waves = 4; break;
     default: c.tiles = tile_ok && !few && !wide_g; c.rows_waves = few && small ? 16 : 4; break;
   }
@@ -1072,6 +1092,8 @@ hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const
 #define DGPRF_FWD_LAUNCH(S, NM) DGPRF_FWD_LAUNCH_W(S, NM, 4)
       if (smalld && nwr == 16) {  // g <= 16 (forward_cfg)
         DGPRF_FWD_LAUNCH_W(true, 1, 16);
+      } else if (smalld && nwr == 8) {
+        DGPRF_FWD_LAUNCH_W(true, 1, 8);
       } else if (smalld) {
         if (notmax == 1) DGPRF_FWD_LAUNCH(true, 1);
         else if (notmax == 2) DGPRF_FWD_LAUNCH(true, 2);

@@ -77,6 +77,7 @@ extern "C" {
 #define DGPRF_FWD_NO_AGEMM 2
 #define DGPRF_FWD_TILE 3        /* tile kernel (one wave per 16-row tile) whatever the row count */
 #define DGPRF_FWD_ROWS16 4      /* row kernel, 16 waves per 16-row tile (small test sets) */
+#define DGPRF_FWD_ROWS8 5       /* row kernel, 8 waves per 16-row tile (two workgroups per CU) */
 
 /* error codes */
 #define DGPRF_OK 0

@@ -2,6 +2,7 @@
 row kernel) on the config's test-set size (capped at 100k rows)."""
 import os
 import sys
+import time
 
 import torch
 
@@ -30,7 +31,7 @@ E.set_seed(3)
 m = DGP_RF(c["d_in"], c["d_out"], n_hidden_layers=len(c["kinds"]), n_rf=c["n_rf"],
            n_gp=c["n_gp"], likelihood=lik, kernel_type_list=c["kinds"])
 code = {"auto": N.FWD_AUTO, "rows": N.FWD_ROWS, "noagemm": N.FWD_NO_AGEMM, "tile": N.FWD_TILE,
-        "rows16": N.FWD_ROWS16}
+        "rows16": N.FWD_ROWS16, "rows8": N.FWD_ROWS8}
 pl = m._engine.layout
 flops = nt * sum(2 * (pl.d[l] * pl.n_rf[l] + pl.P[l] * pl.n_gp[l]) for l in range(pl.n_layers))
 for p in paths:
@@ -41,10 +42,13 @@ for p in paths:
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     S = 20
     e0.record()
+    t0 = time.perf_counter()
     for _ in range(S):
         acc.add_sample(build=False)
+    host_us = (time.perf_counter() - t0) * 1e6 / S
     e1.record()
     torch.cuda.synchronize()
+    print(f"  host enqueue {host_us:.1f} us/sample", flush=True)
     us = e0.elapsed_time(e1) * 1e3 / S
     print(f"config {cfg} N_t={nt} path={p}: {us:.1f} us/sample, "
           f"{flops / us / 1e6:.1f} TFLOP/s = {flops / us / 1e6 / 157.3 * 100:.1f} % of fp32 MFMA peak",

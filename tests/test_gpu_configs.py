@@ -25,6 +25,8 @@ from test_gpu_parity import cpu, dev, pack, rel_err, unpack  # noqa: F401
 pytestmark = pytest.mark.gpu
 
 CONFIGS = {
+    2: dict(kinds=["RBF"] * 3, n_rf=[1024] * 3, n_gp=[8, 8, 1], D=8, lik="gaussian", B=64,
+            n_test=500, ftol=5e-5),
     3: dict(kinds=["ARC"] * 3, n_rf=[2048] * 3, n_gp=[9, 9, 1], D=9, lik="gaussian", B=64,
             n_test=500, ftol=5e-5),
     4: dict(kinds=["RBF"] * 4, n_rf=[4096] * 4, n_gp=[30, 30, 30, 10], D=784, lik="softmax", B=32,
@@ -93,16 +95,18 @@ def test_config_forward_and_grad(dev, cfg):
         assert rel_err(G[l], ref[l]) < 2e-4, (cfg, l)
 
 
-@pytest.mark.parametrize("path", ["tile", "rows16", "rows"])
-def test_predictive_paths_small_test_set(dev, path):
-    """Config 3's model on 1,001 test rows (a ragged tile) through the tile kernel (one wave per
-    16-row tile), the 16-wave row kernel (the product choice below 16k rows) and the 4-wave row
-    kernel: per-row log p against the oracle."""
+@pytest.mark.parametrize("cfg", [2, 3])
+@pytest.mark.parametrize("path", ["tile", "rows16", "rows8", "rows"])
+def test_predictive_paths_small_test_set(dev, path, cfg):
+    """Config 3's model (ARC, d 9: 4 k-steps) and config 2's (RBF, d 8: 2 k-steps) on 1,001 test
+    rows (a ragged tile) through the tile kernel (one wave per 16-row tile), the 16-wave row kernel
+    (the product choice below 16k rows), the 8-wave and the 4-wave row kernels: per-row log p
+    against the oracle."""
     from dgprf import _native as N
-    c = CONFIGS[3]
+    c = CONFIGS[cfg]
     m, p = _model(c, 33)
     Xt, Yt = _data(c, 1001, 203)
-    m._engine.set_forward_path({"tile": N.FWD_TILE, "rows16": N.FWD_ROWS16,
+    m._engine.set_forward_path({"tile": N.FWD_TILE, "rows16": N.FWD_ROWS16, "rows8": N.FWD_ROWS8,
                                 "rows": N.FWD_ROWS}[path])
     lp = cpu(m._engine.forward(Xt, Yt, logp=True)["logp"][0])
     ref = O.log_prob(p, O.forward(p, Xt), Yt)
