@@ -218,10 +218,17 @@ def main():
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
+    # DGPRF_BENCH_BACKEND=gloo (with ranks sharing a GPU: local % device_count) rehearses the N > 1
+    # path on a one-GPU box; the driver's multi-GPU runs use nccl (= RCCL), one GPU per rank
+    backend = os.environ.get("DGPRF_BENCH_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count()) if backend == "gloo" else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from dgprf import engine as E
     from dgprf import _native as N
