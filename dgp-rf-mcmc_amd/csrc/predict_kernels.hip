@@ -20,7 +20,10 @@ namespace {
 
 constexpr int NW = DGPRF_WAVES;
 #ifndef DGPRF_ROWS16_WPE
-#define DGPRF_ROWS16_WPE 8
+#define DGPRF_ROWS16_WPE 8  // waves per SIMD the 16-wave row kernel is budgeted for (8: two per CU)
+#endif
+#ifndef DGPRF_ROWS16_CG
+#define DGPRF_ROWS16_CG 1  // 16-feature chunks per fragment-load group in the 16-wave row kernel
 #endif
 constexpr int TR = DGPRF_TILE_ROWS;
 constexpr float LOG_2PI = 1.8378770664093453f;
@@ -68,7 +71,7 @@ __device__ __forceinline__ void layer_partial(const float* __restrict__ om,
                                               float cl, const float* xs, int xst, float* red,
                                               int wave, int lr, int lq,
                                               const float* __restrict__ arow = nullptr) {
-  constexpr int CG = NWR >= 16 ? 1 : ((NWR >= 8 || NOT > 1) ? 2 : 4);
+  constexpr int CG = NWR >= 16 ? DGPRF_ROWS16_CG : ((NWR >= 8 || NOT > 1) ? 2 : 4);
   static_assert(NKS == 2 || NKS == 4 || NKS == 8, "k-step bucket");
   float xf[NKS];
 #pragma unroll
