@@ -1633,13 +1633,13 @@ __global__ __launch_bounds__(UPD_THREADS) void k_step_update(const UpdK a) {
   const float beta = ud.beta;
   const uint32_t quad = (uint32_t)(e0 >> 2);
   if (resample) {  // models/dgp.py:209-210 (ignores M, Appendix A.1)
-    if (XI && ud.xi_resample)
-      m = ld4(ud.xi_resample + cw + e0);
+    if (XI && ud.xi_resample)  // lanes past w_total (the last block's tail) read 0, no access
+      m = bload4(make_rsrc(ud.xi_resample + cw, a.w_total), off);
     else
       m = philox_normal4(a.seed, (uint64_t)t, DGPRF_RNG_RESAMPLE, (uint32_t)chain, quad);
   }
   f4 mn = beta * m - (h * N) * gr;
-  const f4 eps = (XI && ud.xi) ? ld4(ud.xi + cw + e0)
+  const f4 eps = (XI && ud.xi) ? bload4(make_rsrc(ud.xi + cw, a.w_total), off)
                                : philox_normal4(a.seed, (uint64_t)t, DGPRF_RNG_NOISE, (uint32_t)chain, quad);
   mn = mn + sqrtf(2.0f * (1.0f - beta) * T * M) * eps;
   store(a.mom + cw + e0, mn);

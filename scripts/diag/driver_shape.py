@@ -69,3 +69,26 @@ for spg in spgs:
     print(f"K={K} spg={spg}: wall {w * 1e6 / K:.2f} us/step ({K / w:.0f} steps/s), host call "
           f"{statistics.median(hosts) * 1e6:.0f} us, events {statistics.median(devs) * 1e6 / K:.2f} "
           f"us/step, min wall {min(walls) * 1e6 / K:.2f}", flush=True)
+
+# head + rest plans: a short first graph reaches the GPU sooner while the host submits the rest
+from dgprf import _native as N  # noqa: E402
+eng = m._engine
+mk = lambda k: eng.graph(X, Y, B, N_, 0.01, 0.9, 1.0, k, N.SCHED_CONST, 0, 1, False, 0)
+for plan in ([20], [1, 19], [2, 18], [4, 16], [10, 10]):
+    gs = [mk(k) for k in plan]
+    for g in gs:
+        g.launch()
+    walls = []
+    for _ in range(trials):
+        sync()
+        sync()
+        t0 = time.perf_counter()
+        eng.build_omega()
+        for g in gs:
+            g.launch()
+        sync()
+        sync()
+        walls.append(time.perf_counter() - t0)
+    w = statistics.median(walls)
+    print(f"plan {plan}: wall {w * 1e6 / K:.2f} us/step (min {min(walls) * 1e6 / K:.2f}, "
+          f"first {walls[0] * 1e6 / K:.2f})", flush=True)
