@@ -61,7 +61,7 @@ struct FOut {
 // MFMA chains are independent; cos and sin products accumulate in separate chains.  G1 (g == 1):
 // the W^T Phi^T product is a per-lane dot product (VALU) reduced over the 4 lane groups, instead of
 // a 16x16 MFMA tile that would be 15/16 padding.
-// NKS: k-steps of A = Omega^T x when SMALLD (2, 4 or 8 >= ceil(d / 4), picked per layer by the
+// NKS: k-steps of A = Omega^T x when SMALLD (2, 3, 4 or 8 >= ceil(d / 4), picked per layer by the
 // caller): compile-time, so the Omega loads and A-tile MFMAs carry no per-k-step branch (a runtime
 // count put every load and MFMA behind its own branch and wait: ≈2 us per chunk group on config 3);
 // k-steps past d load zeros (out-of-range buffer offsets) against zero x fragments.
@@ -72,7 +72,7 @@ __device__ __forceinline__ void layer_partial(const float* __restrict__ om,
                                               int wave, int lr, int lq,
                                               const float* __restrict__ arow = nullptr) {
   constexpr int CG = NWR >= 16 ? DGPRF_ROWS16_CG : ((NWR >= 8 || NOT > 1) ? 2 : 4);
-  static_assert(NKS == 2 || NKS == 4 || NKS == 8, "k-step bucket");
+  static_assert(NKS == 2 || NKS == 3 || NKS == 4 || NKS == 8, "k-step bucket");
   float xf[NKS];
 #pragma unroll
   for (int ks = 0; ks < NKS; ++ks) xf[ks] = (SMALLD && 4 * ks < d) ? xs[lr * xst + 4 * ks + lq] : 0.f;
@@ -230,8 +230,10 @@ void k_forward_rows(
   do {                                                                                          \
     if (!SD || d > 16)                                                                          \
       layer_partial<SD, NT, RB, G1_, NWR, 8>(om, W, R, d, g, cl, xs, LD.xst, red, wave, lr, lq, arow); \
-    else if (d > 8)                                                                             \
+    else if (d > 12)                                                                            \
       layer_partial<SD, NT, RB, G1_, NWR, 4>(om, W, R, d, g, cl, xs, LD.xst, red, wave, lr, lq, arow); \
+    else if (d > 8)                                                                             \
+      layer_partial<SD, NT, RB, G1_, NWR, 3>(om, W, R, d, g, cl, xs, LD.xst, red, wave, lr, lq, arow); \
     else                                                                                        \
       layer_partial<SD, NT, RB, G1_, NWR, 2>(om, W, R, d, g, cl, xs, LD.xst, red, wave, lr, lq, arow); \
   } while (0)
@@ -968,6 +970,18 @@ extern "C" int dgprf_debug_read_pred_stamps(unsigned long long* host, long long 
 
 namespace dgprf {
 
+// compute units of the current device (queried once; 256 on MI355X)
+static int device_cus() {
+  static const int cus = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+      v = 256;
+    return v;
+  }();
+  return cus;
+}
+
 ForwardCfg forward_cfg(const dgprf_plan_t& pl, int64_t n) {
   ForwardCfg c;
   // wide first layer (d_1 > 32, e.g. 784 pixels): A_1 = X Omega_1 by the tiled GEMM
@@ -1000,7 +1014,12 @@ ForwardCfg forward_cfg(const dgprf_plan_t& pl, int64_t n) {
     case DGPRF_FWD_ROWS16: c.tiles = false; c.rows_waves = small ? 16 : 4; break;
     case DGPRF_FWD_ROWS8: c.tiles = false; c.rows_waves = small ? 8 : 4; break;
     case DGPRF_FWD_TILE: c.tiles = tile_ok; c.rows_waves = 4; break;
-    default: c.tiles = tile_ok && !few && !wide_g; c.rows_waves = few && small ? 16 : 4; break;
+    // small sets: 16 waves per tile while every tile has a CU of its own; past that (config 3:
+    // 286 tiles) two 8-wave workgroups share a CU (4,573 rows: 43.1 vs 47.8 us with 16 waves)
+    default:
+      c.tiles = tile_ok && !few && !wide_g;
+      c.rows_waves = few && small ? ((n + TR - 1) / TR > device_cus() ? 8 : 16) : 4;
+      break;
   }
   // chunks are whole 64-row tile-kernel workgroups: every wave of the last workgroup reads its 16
   // A_1 rows (rows past n included, their outputs discarded), so the scratch covers align64 rows

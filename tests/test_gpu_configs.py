@@ -100,7 +100,7 @@ def test_config_forward_and_grad(dev, cfg):
 def test_predictive_paths_small_test_set(dev, path, cfg):
     """Config 3's model (ARC, d 9: 4 k-steps) and config 2's (RBF, d 8: 2 k-steps) on 1,001 test
     rows (a ragged tile) through the tile kernel (one wave per 16-row tile), the 16-wave row kernel
-    (the product choice below 16k rows), the 8-wave and the 4-wave row kernels: per-row log p
+    (the product choice below 16k rows while the tiles fit the CUs), the 8-wave (past that) and the 4-wave row kernels: per-row log p
     against the oracle."""
     from dgprf import _native as N
     c = CONFIGS[cfg]
