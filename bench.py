@@ -61,13 +61,26 @@ def cpu_model():
     return None
 
 
-def cpu_baseline(seconds):
+def cpu_threads():
+    """BLAS threads numpy actually runs with (threadpoolctl), and the reason for that count."""
+    try:
+        from threadpoolctl import threadpool_info
+        n = max([int(i.get("num_threads", 1)) for i in threadpool_info()
+                 if i.get("user_api") == "blas"] or [1])
+    except Exception:
+        n = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    return n
+
+
+def cpu_baseline(runs=5, warm=50, timed=1000, pred_samples=5):
     """The reference algorithm, op for op, on the host (oracle/dgp_oracle.py in float32 numpy):
-    TensorFlow is not installed here or on the GPU box, so this restatement is the CPU proxy."""
+    TensorFlow is not installed here or on the GPU box, so this restatement is the CPU proxy.
+    BASELINE.md §3 protocol: `warm` warm-up steps then `timed` timed steps, median of `runs` runs;
+    predictive: `pred_samples` full N_test = 1e5-row samples (in 10k-row chunks)."""
     from oracle import dgp_oracle as O
     rng = np.random.default_rng(0)
     f32 = np.float32
-    d, R, g = [8, 8, 8], CFG["n_rf"], CFG["n_gp"]
+    R, g = CFG["n_rf"], CFG["n_gp"]
     p = O.Params(8, 1, [R] * 3, g, ["RBF"] * 3, "gaussian", False, rng=rng,
                  lik_log_var=np.log(CFG["variance"]), dtype=np.float32)
     n_data = 200_000   # host copy of the synthetic regression data (same distribution)
@@ -77,28 +90,41 @@ def cpu_baseline(seconds):
     Y = ((Y - Y.mean()) / Y.std()).astype(f32)
     m = [rng.standard_normal(w.shape).astype(f32) for w in p.W]
     N, B = CFG["N"], CFG["B"]
-    steps, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        idx = rng.integers(0, n_data, B)
-        xi = [rng.standard_normal(w.shape).astype(f32) for w in p.W]
-        m = O.sgmcmc_step(p, m, X[idx], Y[idx], f32(N), f32(CFG["lr"]), f32(CFG["beta"]),
-                          f32(CFG["T"]), [f32(1.0)] * 3, xi)
-        steps += 1
-    step_rate = steps / (time.perf_counter() - t0)
-    # predictive: forward + log p + se of a 10,000-row slice, scaled to N_test = 1e5 rows
-    Xt = rng.standard_normal((10_000, 8)).astype(f32)
-    Yt = rng.standard_normal((10_000, 1)).astype(f32)
-    reps, t0 = 0, time.perf_counter()
-    while reps < 3 or time.perf_counter() - t0 < min(5.0, seconds / 3):
-        O.eval_log_likelihood_and_se(p, Xt, Yt)
-        reps += 1
-    pred_rate = reps / (time.perf_counter() - t0) / (CFG["N_test"] / 10_000)
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    return {"value": round(step_rate, 2), "unit": "steps/s", "cores": threads, "kind": "port",
+
+    def steps(k):
+        nonlocal m
+        for _ in range(k):
+            idx = rng.integers(0, n_data, B)
+            xi = [rng.standard_normal(w.shape).astype(f32) for w in p.W]
+            m = O.sgmcmc_step(p, m, X[idx], Y[idx], f32(N), f32(CFG["lr"]), f32(CFG["beta"]),
+                              f32(CFG["T"]), [f32(1.0)] * 3, xi)
+
+    rates = []
+    for _ in range(runs):
+        steps(warm)
+        t0 = time.perf_counter()
+        steps(timed)
+        rates.append(timed / (time.perf_counter() - t0))
+    step_rate = float(np.median(rates))
+    Xt = rng.standard_normal((CFG["N_test"], 8)).astype(f32)
+    Yt = rng.standard_normal((CFG["N_test"], 1)).astype(f32)
+    t0 = time.perf_counter()
+    for _ in range(pred_samples):
+        for i in range(0, CFG["N_test"], 10_000):
+            O.eval_log_likelihood_and_se(p, Xt[i:i + 10_000], Yt[i:i + 10_000])
+    pred_rate = pred_samples / (time.perf_counter() - t0)
+    return {"value": round(step_rate, 2), "unit": "steps/s", "cores": cpu_threads(), "kind": "port",
             "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
-            "sample": f"{steps} SGHMC steps of config 2 (B=200, L=3, n_rf=1024, float32 numpy "
-                      f"op-for-op restatement of models/dgp.py:184-216, injected N(0,1) noise); "
-                      f"predictive on a 10k-row slice scaled to 1e5 rows",
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+            "threads_note": "BLAS threads numpy runs with (threadpoolctl); on the GPU box the job's "
+                            "CPU share is 16 (OMP_NUM_THREADS=16 set by the harness) while "
+                            "os.cpu_count() reports the whole host",
+            "protocol": f"{warm} warm-up + {timed} timed steps, median of {runs} runs "
+                        f"({', '.join(f'{r:.1f}' for r in rates)} steps/s); predictive "
+                        f"{pred_samples} full samples",
+            "sample": "SGHMC steps of config 2 (B=200, L=3, n_rf=1024, float32 numpy op-for-op "
+                      "restatement of models/dgp.py:184-216, injected N(0,1) noise); predictive: "
+                      "forward + log p + se of all 1e5 test rows per sample",
             "predictive_samples_per_s": round(pred_rate, 4),
             "note": "BLAS matmuls use the listed threads; numpy elementwise/trig is single-threaded"}
 
@@ -138,9 +164,8 @@ def rocprof_avg_us(prefix):
 def bench_config(cfg, dev, rank, world, barrier_sync, max_over_ranks, steps):
     """Steps/s and predictive samples/s of BASELINE config 3, 4 or 5 (dgprf.data.CONFIGS): the full
     model shape on synthetic data of the config's size, one chain per GPU, graph-replayed steps."""
-    from dgprf import engine as E
     from dgprf.data import CONFIGS, classification_data, regression_data
-    from dgprf.distributed import rank_seed
+    from dgprf.distributed import chain_model, rank_seed
     from dgprf.predictive import PredictiveLSE
     from likelihoods import Gaussian, Softmax
     from models.dgp import DGP_RF
@@ -154,9 +179,10 @@ def bench_config(cfg, dev, rank, world, barrier_sync, max_over_ranks, steps):
         X, Y, a = regression_data(n, c["d_in"], seed=0, device=dev)
         Xt, Yt, _ = regression_data(nt, c["d_in"], seed=1, device=dev, a=a)
         lik = Gaussian(variance=c["variance"])
-    E.set_seed(rank_seed(20 + cfg, rank))
-    m = DGP_RF(c["d_in"], c["d_out"], n_hidden_layers=len(c["kinds"]), n_rf=c["n_rf"],
-               n_gp=c["n_gp"], likelihood=lik, kernel_type_list=c["kinds"])
+    # one model (z, hyper-parameters) on every rank; the rank folds only into its chain's state
+    m = chain_model(lambda: DGP_RF(c["d_in"], c["d_out"], n_hidden_layers=len(c["kinds"]),
+                                   n_rf=c["n_rf"], n_gp=c["n_gp"], likelihood=lik,
+                                   kernel_type_list=c["kinds"]), 20 + cfg, rank)
     m.precond_update(None, n, precond_type="identity")
     run = dict(batch_size=c["batch"], lr=c["lr"], momentum_decay=c["beta"], temperature=c["T"],
                steps_per_graph=100, perm_seed=rank_seed(cfg, rank))
@@ -208,7 +234,7 @@ def main():
     ap.add_argument("--pred-samples", type=int, default=20)
     ap.add_argument("--multi-chains", type=int, default=64)
     ap.add_argument("--full-bayes-steps", type=int, default=2000)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-runs", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-reps", type=int, default=200)
     ap.add_argument("--other-configs", type=int, default=1)
@@ -233,7 +259,7 @@ def main():
     from dgprf import engine as E
     from dgprf import _native as N
     from dgprf.data import regression_data
-    from dgprf.distributed import rank_seed
+    from dgprf.distributed import chain_model, rank_seed
     from dgprf.predictive import PredictiveLSE
     from likelihoods import Gaussian
     from models.regression_model import RegressionDGP
@@ -254,9 +280,12 @@ def main():
     N_, B = CFG["N"], CFG["B"]
     X, Y, a = regression_data(N_, CFG["D"], seed=0, device=dev)
     Xt, Yt, _ = regression_data(CFG["N_test"], CFG["D"], seed=1, device=dev, a=a)
-    E.set_seed(rank_seed(2, rank))
-    model = RegressionDGP(CFG["D"], 1, n_hidden_layers=CFG["L"], n_rf=CFG["n_rf"],
-                          n_gp=CFG["n_gp"], likelihood=Gaussian(variance=CFG["variance"]))
+    # one posterior: z / hyper-parameters from the rank-independent model seed on every rank,
+    # the rank folded only into this chain's noise key, W init and momenta
+    model = chain_model(lambda: RegressionDGP(CFG["D"], 1, n_hidden_layers=CFG["L"],
+                                              n_rf=CFG["n_rf"], n_gp=CFG["n_gp"],
+                                              likelihood=Gaussian(variance=CFG["variance"])),
+                        2, rank)
     model.precond_update(None, N_, precond_type="identity")
     run = dict(batch_size=B, lr=CFG["lr"], momentum_decay=CFG["beta"], temperature=CFG["T"],
                steps_per_graph=args.steps_per_graph, perm_seed=rank_seed(0, rank))
@@ -407,7 +436,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.cpu_seconds)
+        cpu = cpu_baseline(runs=args.cpu_runs)
 
     if rank == 0:
         line = {

@@ -46,7 +46,6 @@ StepDev make_step_dev(const dgprf_plan_t& pl, const dgprf_chain_t& ch, const dgp
   sd.hyp = ch.hyp;
   sd.hmom = ch.hmom;
   sd.hmass = ch.hmass;
-  sd.xb_sel = 0;
   return sd;
 }
 
@@ -106,29 +105,15 @@ int check_step(const dgprf_step_t* st) {
 }
 
 // [gather rows] fwd for every layer, bwd in reverse, then the update.  prep_gather: gather this
-// step's minibatch rows first; gather_next: the step gathers step t+1's rows (graph replays, where
-// the next step is known to follow).
-// W-only steps with plan.fused_update have no update kernel: the backward of layer l updates
-// W_{l+2} in extra workgroups, W_1's update is either applied by the flush kernel (defer0 = false)
-// or left pending for the next step's layer-1 forward (defer0; that step has pend0), and step
-// t+1's rows go to the other gathered-rows buffer (sd.xb_sel alternates).  Otherwise one update
-// kernel sums the gW partials and updates every W (and the full-Bayes hyper-parameters).
+// step's minibatch rows first; gather_next: the update kernel gathers step t+1's rows (graph
+// replays, where the next step is known to follow).  The update kernel sums the gW partials and
+// updates every W (and the full-Bayes hyper-parameters).
 hipError_t enqueue_step(const dgprf_plan_t& pl, const StepDev& sd, const UpdateDev& ud,
-                        hipStream_t s, bool prep_gather = true, bool gather_next = false,
-                        bool pend0 = false, bool defer0 = false) {
+                        hipStream_t s, bool prep_gather = true, bool gather_next = false) {
   hipError_t e = hipSuccess;
   if (prep_gather) e = dgprf::launch_gather(pl, sd, s);
   // random_fixed=False layers: this step's Omega from fresh z (layers/rf_layers.py:39-41)
   if (e == hipSuccess && pl.fresh_z) e = dgprf::launch_fresh_omega(pl, sd, s);
-  if (pl.fused_update && !sd.full_bayes && !ud.grad_only) {
-    for (int l = 0; l < pl.n_layers && e == hipSuccess; ++l)
-      e = dgprf::launch_step_fwd(pl, sd, l, s, &ud, l == 0 && pend0);
-    for (int l = pl.n_layers - 1; l >= 0 && e == hipSuccess; --l)
-      e = dgprf::launch_step_bwd(pl, sd, l, s, &ud, gather_next);
-    if (e == hipSuccess && !(defer0 && pl.fused_update == 1))
-      e = dgprf::launch_layer_update(pl, sd, ud, 0, s);
-    return e;
-  }
   for (int l = 0; l < pl.n_layers && e == hipSuccess; ++l) e = dgprf::launch_step_fwd(pl, sd, l, s);
   for (int l = pl.n_layers - 1; l >= 0 && e == hipSuccess; --l)
     e = dgprf::launch_step_bwd(pl, sd, l, s);
@@ -174,8 +159,7 @@ int dgprf_plan_init(dgprf_plan_t* pl) {
   if (pl->d_in < 1 || pl->d_out < 1 || pl->batch < 1 || pl->n_chains < 1) return DGPRF_E_SHAPE;
   if (pl->likelihood != DGPRF_LIK_GAUSSIAN && pl->likelihood != DGPRF_LIK_SOFTMAX) return DGPRF_E_ARG;
   if (pl->fwd_path < DGPRF_FWD_AUTO || pl->fwd_path > DGPRF_FWD_ROWS8 || pl->agemm_chunk_rows < 0 ||
-      (pl->fuse_update != 0 && pl->fuse_update != 1) || pl->fresh_z < 0 ||
-      (pl->fresh_z >> L) != 0)
+      pl->fresh_z < 0 || (pl->fresh_z >> L) != 0)
     return DGPRF_E_ARG;
   for (int l = 0; l < L; ++l) {
     if (pl->kind[l] != DGPRF_RBF && pl->kind[l] != DGPRF_ARC) return DGPRF_E_ARG;
@@ -261,17 +245,11 @@ int dgprf_plan_init(dgprf_plan_t* pl) {
   ws = align4(ws + (int64_t)B * pl->d_in);
   pl->yb_off = ws;
   ws = align4(ws + (int64_t)B * pl->yb_cols);
-  pl->xb_alt_off = ws;
-  ws = align4(ws + (int64_t)B * pl->d_in);
-  pl->yb_alt_off = ws;
-  ws = align4(ws + (int64_t)B * pl->yb_cols);
   pl->omf_off = -1;
   if (pl->fresh_z) {
     pl->omf_off = ws;
     ws = align4(ws + om);
   }
-  pl->tick_off = ws;  // one 128-byte line per slice: tickets of different slices never share a
-  ws = align4(ws + DGPRF_NS_MAX * 32);  // line (same-line atomics serialise at the memory side)
   // wide first layer: A_1 = X Omega_1 is one tiled GEMM per step (32-row tiles) instead of a
   // d-long dependent k-step loop inside every forward / backward chunk
   pl->a0_off = -1;
@@ -281,22 +259,6 @@ int dgprf_plan_init(dgprf_plan_t* pl) {
   }
   pl->ws_chain = ws;
   pl->ws_total = ws * pl->n_chains;
-  // fused update (W-only steps): layer 1's slice of W (both halves) fits the forward's LDS staging
-  // (<= 4096 floats: 4 float4 per thread), whole float4 runs per half, <= 16 row tiles (one burst
-  // of partial loads), a narrow first layer (no A_1 GEMM) and 32-bit buffer offsets
-  // 2: W_{l+2} by extra workgroups of layer l's backward, W_1 by its own small kernel each step;
-  // 1: as 2, and W_1's update can also wait for the next step's forward (its slice of W_1 fits
-  // the forward's LDS staging, <= 4096 floats; whole float4 runs per half; narrow layer 1)
-  {
-    const int h0 = pl->kind[0] == DGPRF_RBF ? 2 : 1;
-    const int64_t slice = (int64_t)h0 * 64 * pl->cpw[0] * pl->n_gp[0];
-    const bool ok = pl->fuse_update == 1 && pl->n_row_tiles <= 16 &&
-                    pl->ws_chain * pl->n_chains < ((int64_t)1 << 29) &&
-                    pl->w_total * pl->n_chains < ((int64_t)1 << 29);
-    const bool pend = slice <= 4096 && pl->n_gp[0] <= 16 &&
-                      ((int64_t)pl->n_rf[0] * pl->n_gp[0]) % 4 == 0 && pl->a0_off < 0;
-    pl->fused_update = ok ? (pend ? 1 : 2) : 0;
-  }
   pl->initialised = 1;
   return DGPRF_OK;
 }
@@ -372,8 +334,11 @@ int dgprf_graph_create_sghmc(dgprf_graph_handle* out, const dgprf_plan_t* plan,
   hipStream_t cs;
   if (hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess) return DGPRF_E_HIP;
   if (plan->a0_off >= 0) {  // library GEMM state (handle, tuned algorithm) before capture
+    // The warm-up writes the workspace's A_1 on `cs`, which is not ordered after the caller's
+    // stream: let every earlier kernel (e.g. gradients still reading A_1) finish first.
     const StepDev sd0 = make_step_dev(*plan, *chain, *batch, step->step_offset);
-    if (dgprf::launch_step_agemm(*plan, sd0, cs) != hipSuccess || hipStreamSynchronize(cs) != hipSuccess) {
+    if (hipDeviceSynchronize() != hipSuccess || dgprf::launch_step_agemm(*plan, sd0, cs) != hipSuccess ||
+        hipStreamSynchronize(cs) != hipSuccess) {
       (void)hipStreamDestroy(cs);
       return DGPRF_E_HIP;
     }
@@ -382,15 +347,10 @@ int dgprf_graph_create_sghmc(dgprf_graph_handle* out, const dgprf_plan_t* plan,
   dgprf_step_t st = *step;
   st.grad_only = 0;
   const UpdateDev ud = make_update_dev(st);
-  const bool fused = plan->fused_update && !st.full_bayes;
   for (int k = 0; k < steps_per_graph && e == hipSuccess; ++k) {
     StepDev sd = make_step_dev(*plan, *chain, *batch, st.step_offset + k);
     sd.full_bayes = st.full_bayes != 0;
-    sd.xb_sel = fused ? (k & 1) : 0;
-    const bool more = k + 1 < steps_per_graph;
-    const bool defer = plan->fused_update == 1;  // W_1's update may wait for the next forward
-    e = enqueue_step(*plan, sd, ud, cs, k == 0, more, /*pend0=*/defer && k > 0,
-                     /*defer0=*/defer && more);
+    e = enqueue_step(*plan, sd, ud, cs, k == 0, k + 1 < steps_per_graph);
   }
   if (e == hipSuccess) e = dgprf::launch_advance(chain->step, steps_per_graph, cs);
   hipGraph_t g = nullptr;
@@ -450,14 +410,12 @@ int dgprf_profile_step(const dgprf_plan_t* plan, const dgprf_chain_t* chain,
   for (int rep = 0; rep < reps && e == hipSuccess; ++rep) {
     const StepDev sd = make_step_dev(*plan, *chain, *batch, st.step_offset);
     e = dgprf::launch_gather(*plan, sd, s);
-    const bool fused = plan->fused_update != 0;
     for (int j = 0; j < K && e == hipSuccess; ++j) {
       const int kk = j < L ? j : (j < 2 * L ? L + (2 * L - 1 - j) : 2 * L);
       e = hipEventRecord(ev[2 * kk], s);
       if (e != hipSuccess) break;
-      if (kk < L) e = dgprf::launch_step_fwd(*plan, sd, kk, s, fused ? &ud : nullptr);
-      else if (kk < 2 * L) e = dgprf::launch_step_bwd(*plan, sd, kk - L, s, fused ? &ud : nullptr);
-      else if (fused) e = dgprf::launch_layer_update(*plan, sd, ud, 0, s);  // W_1 (the flush)
+      if (kk < L) e = dgprf::launch_step_fwd(*plan, sd, kk, s);
+      else if (kk < 2 * L) e = dgprf::launch_step_bwd(*plan, sd, kk - L, s);
       else e = dgprf::launch_step_update(*plan, sd, ud, nullptr, s);
       if (e == hipSuccess) e = hipEventRecord(ev[2 * kk + 1], s);
     }

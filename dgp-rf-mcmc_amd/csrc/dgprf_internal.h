@@ -25,8 +25,6 @@ struct StepDev {
   float* hyp;
   float* hmom;
   const float* hmass;
-  // which gathered-rows buffer this step reads (0: xb/yb, 1: xb_alt/yb_alt)
-  int32_t xb_sel;
 };
 
 struct UpdateDev {
@@ -86,20 +84,11 @@ inline void set_lds_limit(const void* fn, size_t bytes) {
   if (bytes > 65536) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
-// Forward / backward of one layer.  With the fused update (plan.fused_update; `ud` non-null):
-//   fwd(layer 0, pend): first applies the previous step's pending W_1 update (its gW partials are
-//     still in the workspace) to the workgroup's feature slice, computes with the new W_1, and the
-//     slice's last-arriving workgroup stores it;
-//   bwd(layer l): extra workgroups update W_{l+1} from its gW partials (l + 1 < L), and, when
-//     gather_next, the last layer's backward gathers step t+1's rows into the other buffer.
-hipError_t launch_step_fwd(const dgprf_plan_t& pl, const StepDev& sd, int layer, hipStream_t s,
-                           const UpdateDev* ud = nullptr, bool pend = false);
-hipError_t launch_step_bwd(const dgprf_plan_t& pl, const StepDev& sd, int layer, hipStream_t s,
-                           const UpdateDev* ud = nullptr, bool gather_next = false);
-// Fused mode: the SGHMC update of W_{layer+1} alone, from its gW partials (the flush of the
-// deferred layer-1 update at the end of a call / graph).
-hipError_t launch_layer_update(const dgprf_plan_t& pl, const StepDev& sd, const UpdateDev& ud,
-                               int layer, hipStream_t s);
+// Forward / backward of one layer of the step (k_step_fwd / k_step_bwd).
+hipError_t launch_step_fwd(const dgprf_plan_t& pl, const StepDev& sd, int layer, hipStream_t s);
+hipError_t launch_step_bwd(const dgprf_plan_t& pl, const StepDev& sd, int layer, hipStream_t s);
+// Sums the gW partials, adds the prior term and applies the SGHMC update (or writes the gradient);
+// gather_next: extra workgroups gather step t+1's minibatch rows.
 hipError_t launch_step_update(const dgprf_plan_t& pl, const StepDev& sd, const UpdateDev& ud,
                               const float* grad_in, hipStream_t s, bool gather_next = false);
 // (sd.full_bayes: the same launch also runs the hyper-parameter workgroups — their gradients or

@@ -1,0 +1,3 @@
+// step_fwd_k0.hip — k_step_fwd instances with KS = 0 A-tile k-steps (d > 32: A_1 precomputed).
+#define DGPRF_KS 0
+#include "step_fwd_impl.h"

@@ -22,7 +22,7 @@ RNG_NOISE, RNG_RESAMPLE, RNG_Z, RNG_W, RNG_MOMENTS = 1, 2, 3, 4, 5
 RNG_HYPER, RNG_HYPER_RESAMPLE = 6, 7
 HYP_KERNEL, HYP_LIK, HYP_MEAN = 1, 2, 4
 HMASS = 32  # hmass slots: log_amp l -> l, log_inv_ls l -> 8 + l, mean l -> 16 + l, lik_log_var -> 24
-ABI_VERSION = 4
+ABI_VERSION = 5
 FWD_AUTO, FWD_ROWS, FWD_NO_AGEMM, FWD_TILE, FWD_ROWS16, FWD_ROWS8 = 0, 1, 2, 3, 4, 5
 
 E_ARG, E_SHAPE, E_HIP, E_PLAN = -1, -2, -3, -4
@@ -42,7 +42,7 @@ class Plan(ctypes.Structure):
         ("likelihood", _i32), ("batch", _i32), ("n_chains", _i32),
         ("kind", _i32 * _L), ("n_rf", _i32 * _L), ("n_gp", _i32 * _L),
         ("hyp_flags", _i32), ("hyp_per_chain", _i32), ("ard", _i32 * _L),
-        ("fwd_path", _i32), ("agemm_chunk_rows", _i32), ("fuse_update", _i32), ("fresh_z", _i32),
+        ("fwd_path", _i32), ("agemm_chunk_rows", _i32), ("fresh_z", _i32),
         ("initialised", _i32),
         ("d", _i32 * _L), ("P", _i32 * _L), ("ns", _i32 * _L), ("cpw", _i32 * _L),
         ("n_row_tiles", _i32), ("n_rt_pad", _i32),
@@ -52,8 +52,7 @@ class Plan(ctypes.Structure):
         ("omega_total", _i64), ("w_total", _i64), ("hyp_total", _i64), ("der_total", _i64),
         ("ws_chain", _i64), ("ws_total", _i64), ("hpp_off", _i64 * _L), ("hpl_off", _i64),
         ("xb_off", _i64), ("yb_off", _i64),
-        ("yb_cols", _i32), ("fused_update", _i32), ("a0_off", _i64),
-        ("xb_alt_off", _i64), ("yb_alt_off", _i64), ("omf_off", _i64), ("tick_off", _i64),
+        ("yb_cols", _i32), ("pad0", _i32), ("a0_off", _i64), ("omf_off", _i64),
     ]
 
 

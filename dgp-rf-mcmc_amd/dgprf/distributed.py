@@ -26,6 +26,26 @@ def rank_seed(seed, rank):
     return z ^ (z >> 31)
 
 
+def chain_model(build, model_seed, rank):
+    """This rank's chain of ONE posterior.
+
+    The model — RF frequencies z, kernel / likelihood hyper-parameters, everything `build()` draws
+    at construction (layers/rf_layers.py:21-22) — comes from the rank-independent `model_seed`, so
+    every rank samples the same fixed-z model, as the reference scores successive samples of one
+    model (experiments/utils_training.py:62-65,79-85).  Only the chain's own state folds the rank:
+    the Philox key of its step noise, its W initialisation (layers/GP_weight_layers.py:9) and the
+    momenta drawn later by precond_update (models/dgp.py:235-240)."""
+    from . import _native as N
+    from . import engine as E
+    E.set_seed(model_seed)
+    m = build()
+    eng = m._engine
+    E.set_seed(rank_seed(model_seed, rank))
+    eng.seed = E.engine_key()
+    E.normal(None, N.RNG_W, out=eng.theta)
+    return m
+
+
 def gather_accumulators(m, s, e, S_local, group=None):
     """All-gather per-rank LSE accumulators [C, n] -> [W*C, n] in rank order, and sum S."""
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:

@@ -120,10 +120,6 @@ class ModelSpec:
 
 class Engine:
     MAX_GRAPHS = 8  # instantiated step graphs kept per engine (LRU)
-    # request plan.fuse_update (set before the first step of a batch size): the SGHMC update inside
-    # the forward / backward kernels instead of one update kernel per step — correct, but measured
-    # no faster on config 2 and slower on config 3 / many chains, so off by default
-    fused_update = False
 
     def __init__(self, spec, n_chains=1, dev=None, seed=None, per_chain_hyp=None):
         """per_chain_hyp: every chain owns its kernel / likelihood hyper-parameters (and Omega),
@@ -232,8 +228,7 @@ class Engine:
         key = (int(B), int(fresh_z))
         if key not in self._ws:
             pl = self.spec.plan(key[0], self.C, self.per_chain_hyp)
-            if self.fused_update or fresh_z:
-                pl.fuse_update = int(bool(self.fused_update))  # request (plan_init grants or not)
+            if fresh_z:
                 pl.fresh_z = key[1]
                 N.call("dgprf_plan_init", ctypes.byref(pl))
             ws = torch.zeros(max(pl.ws_total, 4), dtype=_F32, device=self.dev)
@@ -395,8 +390,12 @@ class Engine:
             g = self._graphs.pop(key)  # most recently used last
             self._graphs[key] = g
             return g
-        while len(self._graphs) >= self.MAX_GRAPHS:  # bounded: evict the least recently used
-            self._graphs.pop(next(iter(self._graphs)))
+        if len(self._graphs) >= self.MAX_GRAPHS:
+            # bounded: evict the least recently used.  Replays are asynchronous, so the stream
+            # drains before an evicted graph's executable can be destroyed (_Graph.__del__).
+            torch.cuda.current_stream(self.dev).synchronize()
+            while len(self._graphs) >= self.MAX_GRAPHS:
+                self._graphs.pop(next(iter(self._graphs)))
         pl, ws = self.plan_ws(batch_size, fresh_z)
         iters = X_all.shape[0] // int(batch_size)
         ch = self.chain_struct(ws)

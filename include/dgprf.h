@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define DGPRF_ABI_VERSION 4
+#define DGPRF_ABI_VERSION 5
 
 #define DGPRF_MAX_LAYERS 8
 #define DGPRF_MAX_G 64        /* max latent GPs per layer (n_gp[l]) */
@@ -122,7 +122,6 @@ typedef struct dgprf_plan {
   int32_t fwd_path;        /* DGPRF_FWD_* (0 = AUTO) */
   int32_t agemm_chunk_rows; /* wide first layer: rows of A_1 per dgprf_forward chunk (0 = as many as
                                fit 64M floats; otherwise rounded down to a multiple of 64, >= 64) */
-  int32_t fuse_update;     /* 1: request the fused W-only update (see fused_update below) */
   int32_t fresh_z;         /* bit l: layer l draws fresh z ~ N(0,1) every step (random_fixed=False,
                               layers/rf_layers.py:39-41): the step builds that layer's Omega from
                               Philox (seed, sub = step, DGPRF_RNG_Z, tag = 1 + l + 16 chain) into
@@ -155,22 +154,12 @@ typedef struct dgprf_plan {
   int64_t xb_off;                    /* gathered minibatch rows X [B][d_in] (per chain)        */
   int64_t yb_off;                    /* gathered minibatch targets [B][yb_cols] (per chain)    */
   int32_t yb_cols;                   /* g_L (Gaussian) or 1 (softmax label)                    */
-  int32_t fused_update;              /* fuse_update granted for W-only steps (0: one update kernel
-                                        per step).  2: W_{l+2} updated by extra workgroups of layer
-                                        l's backward, W_1 by its own small kernel per step.  1: as 2,
-                                        and in graphs W_1's update is deferred into the next step's
-                                        layer-1 forward (its slice fits the forward's LDS), with a
-                                        flush kernel at the end of a call / graph.               */
+  int32_t pad0;
   int64_t a0_off;                    /* layer 1 with d > 32 (e.g. the 784-wide MNIST input):
                                         A_1 = X Omega_1 [align32(B)][R_1] precomputed by one tiled
                                         MFMA GEMM per step (per chain); -1 when not used          */
-  int64_t xb_alt_off;                /* second gathered-rows buffers (graph steps alternate      */
-  int64_t yb_alt_off;                /*   between the two by step parity)                       */
   int64_t omf_off;                   /* fresh_z != 0: this step's Omega of every layer [omega_total]
                                         (per chain; fresh layers rebuilt each step); -1 otherwise */
-  int64_t tick_off;                  /* [16][32] uint32 arrival tickets of the deferred W_1
-                                        update, one 128-byte line per feature slice (per chain;
-                                        zero between launches)                                   */
 } dgprf_plan_t;
 
 /* Device state of the chains.  Replaces the tf.Variables W and their ad-hoc attributes

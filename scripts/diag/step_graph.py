@@ -1,6 +1,9 @@
-"""Diagnostic: graph-replayed SGHMC steps of config 2 (or another BASELINE config), fused update
-vs the separate update kernel, timed with events over K replayed steps; run under
-`rocprofv3 --kernel-trace --stats` for per-kernel durations."""
+"""Diagnostic: graph-replayed SGHMC steps of config 2 (or another BASELINE config) at one or more
+minibatch sizes, timed with events over K replayed steps; run under
+`rocprofv3 --kernel-trace --stats` for per-kernel durations.
+
+  python scripts/diag/step_graph.py [config] [B1,B2,...] [steps]
+"""
 import os
 import sys
 
@@ -14,9 +17,9 @@ from likelihoods import Gaussian, Softmax  # noqa: E402
 from models.dgp import DGP_RF  # noqa: E402
 
 cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 2
-modes = sys.argv[2].split(",") if len(sys.argv) > 2 else ["fused", "kernel"]
-steps = int(sys.argv[3]) if len(sys.argv) > 3 else 2000
 c = CONFIGS[cfg]
+batches = [int(b) for b in sys.argv[2].split(",")] if len(sys.argv) > 2 else [c["batch"]]
+steps = int(sys.argv[3]) if len(sys.argv) > 3 else 2000
 dev = torch.device("cuda", 0)
 if c["likelihood"] == "softmax":
     X, Y = classification_data(c["n"], c["d_in"], c["d_out"], seed=0, device=dev)
@@ -24,21 +27,24 @@ if c["likelihood"] == "softmax":
 else:
     X, Y, _ = regression_data(c["n"], c["d_in"], seed=0, device=dev)
     lik = Gaussian(variance=c["variance"])
-for mode in modes:
-    E.Engine.fused_update = mode == "fused"
+for B in batches:
     E.set_seed(3)
     m = DGP_RF(c["d_in"], c["d_out"], n_hidden_layers=len(c["kinds"]), n_rf=c["n_rf"],
                n_gp=c["n_gp"], likelihood=lik, kernel_type_list=c["kinds"])
     m.precond_update(None, c["n"], precond_type="identity")
-    run = dict(batch_size=c["batch"], lr=c["lr"], momentum_decay=c["beta"], temperature=c["T"],
-               steps_per_graph=100)
-    m.run_sgmcmc(X, Y, c["n"], 200, **run)
+    spg = 100 if B <= 1024 else 10
+    run = dict(batch_size=B, lr=c["lr"], momentum_decay=c["beta"], temperature=c["T"],
+               steps_per_graph=spg)
+    k = max(spg, steps // spg * spg) if B <= 1024 else max(spg, steps // 10 // spg * spg)
+    m.run_sgmcmc(X, Y, c["n"], 2 * spg, **run)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    m.run_sgmcmc(X, Y, c["n"], steps, **run)
+    m.run_sgmcmc(X, Y, c["n"], k, **run)
     e1.record()
     torch.cuda.synchronize()
-    us = e0.elapsed_time(e1) * 1e3 / steps
-    print(f"config {cfg} {mode}: {us:.2f} us/step ({1e6 / us:.0f} steps/s) "
-          f"plan.fused_update={m._engine.plan_ws(c['batch'])[0].fused_update}", flush=True)
+    us = e0.elapsed_time(e1) * 1e3 / k
+    pl = m._engine.plan_ws(B)[0]
+    print(f"config {cfg} B={B}: {us:.2f} us/step ({1e6 / us:.0f} steps/s), ws {pl.ws_chain * 4 / 1e6:.1f} MB",
+          flush=True)
+    del m

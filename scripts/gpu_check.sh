@@ -3,7 +3,7 @@
 # anything other than success / ordinary test failure (exit 0/1) ends the call.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out
-BENCH_ARGS=${BENCH_ARGS:-"--steps 2000 --warmup 200 --cpu-seconds 10"}
+BENCH_ARGS=${BENCH_ARGS:-"--steps 2000 --warmup 200 --cpu-runs 5"}
 PYTEST_ARGS=${PYTEST_ARGS:-"tests -m gpu -q"}
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
 rc=$?; echo "smoke rc=$rc"; tail -3 gpurun_out/smoke.log

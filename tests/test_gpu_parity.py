@@ -95,17 +95,6 @@ def pack(engine, per_layer):
 CASES = ["rbf2_gauss", "arc_rbf_softmax_cat", "mixed5", "wide_g"]
 
 
-@pytest.fixture(params=["kernel", "fused"])
-def update_path(request):
-    """Both W-only update paths: the per-step update kernel (default) and plan.fuse_update (the
-    update inside the step kernels; granted for these shapes)."""
-    from dgprf import engine as E
-    old = E.Engine.fused_update
-    E.Engine.fused_update = request.param == "fused"
-    yield request.param
-    E.Engine.fused_update = old
-
-
 @pytest.mark.parametrize("n,P,g", [(1000, 2048, 30), (77, 8192, 16), (5, 6, 1), (33, 130, 17)])
 def test_gp_layer_matmul(dev, n, P, g):
     """Stand-alone GPLayer.__call__ (layers/GP_weight_layers.py:11-15) on the MFMA tile kernel:
@@ -192,7 +181,7 @@ def test_potential_grad(dev, golden, name):
 
 @pytest.mark.parametrize("name", CASES)
 @pytest.mark.parametrize("resample", [False, True])
-def test_sghmc_step_injected_noise(dev, update_path, golden, name, resample):
+def test_sghmc_step_injected_noise(dev, golden, name, resample):
     g = golden(name)
     m = model_from_fixture(g)
     eng = m._engine
@@ -212,7 +201,7 @@ def test_sghmc_step_injected_noise(dev, update_path, golden, name, resample):
         assert rel_err(cpu(eng.mom_view(l)), g[f"m1{sfx}_{l}"]) < 1e-4
 
 
-def test_config1_sgld_trajectory(dev, update_path, golden):
+def test_config1_sgld_trajectory(dev, golden):
     """Config 1 (1-layer RBF n_rf=100, mcycle-shaped N=133, full batch): 50 SGLD steps with
     injected noise track the float64 oracle trajectory."""
     from likelihoods import Gaussian
@@ -254,7 +243,7 @@ def test_standalone_update(dev, golden):
         assert rel_err(cpu(eng.mom_view(l)), m1) < 1e-5
 
 
-def test_device_philox_noise_counter(dev, update_path, golden):
+def test_device_philox_noise_counter(dev, golden):
     """The update's in-kernel noise is the Philox stream (seed, sub = step, NOISE, tag = chain)
     indexed by the packed element: a Philox step equals an injected-noise step."""
     g = golden("mixed5")
@@ -322,7 +311,7 @@ def test_epoch_minibatch_rows_bit_exact(dev):
         assert torch.equal(ge, gd), t
 
 
-def test_graph_replay_equals_eager_steps(dev, update_path):
+def test_graph_replay_equals_eager_steps(dev):
     from likelihoods import Gaussian
     from models.regression_model import RegressionDGP
     from dgprf import engine as E
@@ -342,12 +331,11 @@ def test_graph_replay_equals_eager_steps(dev, update_path):
     for _ in range(24):
         b._engine.step(X, Y, n, 0.01, 0.9, 1.0, batch_size=B, mode=2, perm_seed=3)
     assert int(a._engine.step_ctr) == 24 == int(b._engine.step_ctr)
-    assert a._engine.plan_ws(B)[0].fused_update == (update_path == "fused")
     assert torch.equal(a._engine.theta, b._engine.theta)
     assert torch.equal(a._engine.mom, b._engine.mom)
 
 
-def test_graph_fresh_z_random_fixed_false(dev, update_path):
+def test_graph_fresh_z_random_fixed_false(dev):
     """random_fixed=False inside graph-replayed steps (layers/rf_layers.py:39-41): every step draws
     z ~ N(0,1) on the device from Philox (seed, sub = step, RNG_Z, tag = 1 + layer) and builds that
     step's Omega; 3 graph steps equal 3 eager steps of a random_fixed=True twin whose z is set to
@@ -382,7 +370,52 @@ def test_graph_fresh_z_random_fixed_false(dev, update_path):
     assert rel_err(cpu(ea.theta), cpu(eb.theta)) < 1e-5
 
 
-def test_device_cyclical_schedule(dev, update_path):
+def test_graph_fresh_z_two_chains(dev):
+    """random_fixed=False with C = 2 chains in one graph: chain c draws its own z from Philox
+    (seed, sub = step, RNG_Z, tag = 1 + l + 16 c) into its own workspace copy of Omega (chain
+    stride ws_chain).  At T = 0 (no noise) each chain's 3 graph steps equal 3 eager single-chain
+    steps on the same rows (oracle Feistel rows of chain c) with z set to that chain's draws."""
+    from dgprf import _native as N
+    from dgprf import engine as E
+    from oracle import rng as R
+    spec = E.ModelSpec(3, 1, [N.RBF, N.ARC], [32, 24], [4, 1], False, N.LIK_GAUSSIAN)
+    two = E.Engine(spec, 2, seed=4242)
+    two.draw_init()
+    E.normal(None, N.RNG_W, out=two.theta)
+    E.normal(None, N.RNG_MOMENTS, out=two.mom)
+    two.build_omega()
+    n, B, lr, beta, steps = 320, 32, 0.01, 0.9, 3
+    X = torch.randn(n, 3, device=dev)
+    Y = torch.randn(n, 1, device=dev)
+    th0, mo0 = two.theta.clone(), two.mom.clone()
+    two.graph(X, Y, B, n, lr, beta, 0.0, steps, perm_seed=7, fresh_z=0b11).launch()
+    pl, ws = two.plan_ws(B, 0b11)
+    iters = n // B
+    for c in range(2):
+        # the workspace's Omega of chain c is the last step's fresh draw
+        om_ws = ws[c * pl.ws_chain + pl.omf_off:c * pl.ws_chain + pl.omf_off + pl.omega_total]
+        for l in range(2):
+            z = R.philox_normal(pl.d[l] * pl.n_rf[l], two.seed, steps - 1, R.PURPOSE_Z,
+                                tag=1 + l + 16 * c).reshape(pl.d[l], pl.n_rf[l])
+            ref = np.exp(cpu(two.lis_view(l)))[:, None] * z
+            got = cpu(om_ws[pl.omega_off[l]:pl.omega_off[l] + z.size]).reshape(z.shape)
+            assert rel_err(got, ref) < 1e-6, (c, l)
+        one = E.Engine(spec, 1, seed=two.seed)
+        one.hyp.copy_(two.hyp[:one.hyp.numel()])
+        one.theta.copy_(th0[c:c + 1])
+        one.mom.copy_(mo0[c:c + 1])
+        for t in range(steps):
+            for l in range(2):
+                z = R.philox_normal(pl.d[l] * pl.n_rf[l], two.seed, t, R.PURPOSE_Z,
+                                    tag=1 + l + 16 * c)
+                one.z_view(l).copy_(torch.as_tensor(z.reshape(pl.d[l], pl.n_rf[l]),
+                                                    dtype=torch.float32))
+            rows = R.batch_rows(t, B, n, iters, perm_seed=7, chain=c).astype(np.int32)
+            one.step(X, Y, n, lr, beta, 0.0, batch_size=B, mode=N.BATCH_INDEXED, idx=rows)
+        assert rel_err(cpu(one.theta[0]), cpu(two.theta[c])) < 1e-5, c
+
+
+def test_device_cyclical_schedule(dev):
     """DGPRF_SCHED_CYCLICAL: burn-in lr0/T=0 then lr0 * rate^2, T=1 (utils_training.py:47-61)."""
     from likelihoods import Gaussian
     from models.regression_model import RegressionDGP
@@ -410,7 +443,7 @@ def test_device_cyclical_schedule(dev, update_path):
     assert rel_err(cpu(a._engine.theta), cpu(b._engine.theta)) < 1e-5
 
 
-def test_multichain_chain0_matches_single_chain(dev, update_path):
+def test_multichain_chain0_matches_single_chain(dev):
     from dgprf import engine as E
     from dgprf import _native as N
     spec = E.ModelSpec(3, 1, [N.RBF, N.ARC], [32, 48], [4, 1], False, N.LIK_GAUSSIAN)

@@ -25,13 +25,17 @@ pytestmark = pytest.mark.gpu
 CFG2 = dict(kinds=["RBF"] * 3, n_rf=[1024] * 3, n_gp=[8, 8, 1], D=8, variance=0.1)
 
 
-def _config2_model(seed):
-    from dgprf import engine as E
+def _build_config2():
     from likelihoods import Gaussian
     from models.regression_model import RegressionDGP
-    E.set_seed(seed)
     return RegressionDGP(CFG2["D"], 1, n_hidden_layers=3, n_rf=CFG2["n_rf"], n_gp=CFG2["n_gp"],
                          likelihood=Gaussian(variance=CFG2["variance"]))
+
+
+def _config2_model(seed):
+    from dgprf import engine as E
+    E.set_seed(seed)
+    return _build_config2()
 
 
 def _oracle_params(m, W):
@@ -163,17 +167,28 @@ def _free_port():
 def _rank_worker(rank, world, port, q):
     """One rank: 2 chains of its own (rank-keyed draws of W) over the shared test set and model,
     2 samples each; PredictiveLSE.finalize all-gathers the accumulators (gloo: host-staged, two
-    ranks share the one GPU) and runs k_lse_finalize on the stacked [world * 2, n] rows."""
+    ranks share the one GPU) and runs k_lse_finalize on the stacked [world * 2, n] rows.  The
+    model comes from the helper bench.py uses (dgprf.distributed.chain_model): z and the
+    hyper-parameters are gathered and must be bitwise equal on every rank (one posterior)."""
     from dgprf import _native as N
     from dgprf import engine as E
     from dgprf.data import regression_data
-    from dgprf.distributed import rank_seed
+    from dgprf.distributed import chain_model, rank_seed
     from dgprf.predictive import PredictiveLSE
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     Xt, Yt, _ = regression_data(5_003, CFG2["D"], seed=6, device="cuda")
-    m = _config2_model(8)          # same frequencies / hyper-parameters on every rank
+    m = chain_model(_build_config2, 8, rank)
+    eng = m._engine
+    eng.build_omega()
+    for t in (eng.z, eng.hyp, eng.omega):  # one model on every rank
+        parts = [torch.empty_like(t.cpu()) for _ in range(world)]
+        dist.all_gather(parts, t.cpu())
+        assert all(torch.equal(parts[0], p) for p in parts), "ranks built different models"
+    seeds = [None] * world
+    dist.all_gather_object(seeds, (eng.seed, float(eng.theta[0, 0])))
+    assert len(set(seeds)) == world, "every rank's chain needs its own noise key and W init"
     me = _multi_chain_engine(m, 2, seed=rank_seed(1, rank))
     E.set_seed(rank_seed(2, rank))
     acc = PredictiveLSE(me, Xt, Yt)
