@@ -7,6 +7,7 @@
 #include <new>
 
 #include "dgprf_internal.h"
+#include "step_common.h"
 
 namespace {
 
@@ -126,6 +127,7 @@ hipError_t enqueue_step(const dgprf_plan_t& pl, const StepDev& sd, const UpdateD
 int check_full_bayes(const dgprf_plan_t& pl, const dgprf_chain_t& ch) {
   if (!ch.z || !ch.hyp || !ch.hmom || !ch.hmass) return DGPRF_E_ARG;
   if (pl.n_chains > 1 && !pl.hyp_per_chain) return DGPRF_E_ARG;
+  if (pl.rt_per_group > 1 && !pl.rg_full_bayes) return DGPRF_E_SHAPE;
   return DGPRF_OK;
 }
 
@@ -227,7 +229,25 @@ int dgprf_plan_init(dgprf_plan_t* pl) {
     pl->dxp_off[l] = ws;
     ws = align4(ws + (int64_t)DGPRF_NS_MAX * B * pl->n_gp[l - 1]);
   }
-  pl->n_rt_pad = (pl->n_row_tiles + 15) / 16 * 16;
+  // backward row groups: beyond 16 row tiles every workgroup walks ceil(n_rt / 16) row tiles and
+  // keeps its gW in accumulators (k_step_bwd_rg), so the gW partials stay <= 16 rows
+  pl->rt_per_group = 1;
+  pl->rg_full_bayes = 0;
+  pl->pad1 = 0;
+  if (pl->n_row_tiles > 16) {
+    bool ok = true, ok_fb = true;
+    dgprf_sk::RgCfg c;
+    for (int l = 0; l < L; ++l) {
+      ok = ok && dgprf_sk::rg_config(*pl, l, false, c);
+      ok_fb = ok_fb && dgprf_sk::rg_config(*pl, l, true, c);
+    }
+    if (ok) {
+      pl->rt_per_group = (pl->n_row_tiles + 15) / 16;
+      pl->rg_full_bayes = ok_fb ? 1 : 0;
+    }
+  }
+  pl->n_gw_rows = (pl->n_row_tiles + pl->rt_per_group - 1) / pl->rt_per_group;
+  pl->n_rt_pad = (pl->n_gw_rows + 15) / 16 * 16;
   pl->gwp_off = ws;
   ws = align4(ws + (int64_t)pl->n_rt_pad * pl->w_total);
   pl->logp_off = ws;

@@ -78,6 +78,9 @@ struct LayerK {
   int32_t wstage, wsa_off, osa_off, osa_st, kind_rbf, pad_w;
   int32_t main_blocks;  // this layer's (row tile, slice) workgroups
   int32_t pad_m;
+  // row-group backward (k_step_bwd_rg, minibatches of > 16 row tiles): rt_per_rg row tiles per
+  // workgroup, ncw chunk-waves x nrw row-waves, register-prefetched prologue when rg_fast
+  int32_t rt_per_rg, ncw, nrw, rg_fast, gred_off, rg_nit;
 };
 
 // Block -> (row tile, slice): blocks are dealt round-robin over the 8 XCDs, so block b's XCD group
@@ -167,15 +170,28 @@ __device__ __forceinline__ float sum_slices(const float* __restrict__ p, int64_t
   return acc;
 }
 
-__host__ __device__ inline void step_lds(int d, int g, LayerK& a, int& total, int nwb = NW) {
+// LDS layout of one forward / backward workgroup of nwb waves (floats): X tile [TR][xst], the
+// backward's dF and Y tiles [TR][auxst], then `red` — the per-wave reduction rows (F [nwb][TR][GP]
+// in the forward, dX [nwb][TR][DP] in the backward; also the prologue's scratch slots) — then the
+// backward's 64-feature W / Omega staging block when dPhi / dX need them.  Sized to the layer, so
+// small layers leave room for more resident workgroups (large minibatches).
+__host__ __device__ inline void step_lds(LayerK& a, int& total, int nwb, bool bwd, bool dphi) {
+  const int d = a.d, g = a.g;
   a.xst = round4(d) + 1;
   a.aux_off = round4(TR * a.xst);
   a.auxst = g + 1;
-  a.red_off = a.aux_off + 2 * round4(TR * a.auxst);  // dF tile + Y tile
-  // backward: the workgroup's 64-feature block of W_l ([2][64*g] raw) and Omega_l ([64][OST])
-  a.stg_off = a.red_off + nwb * TR * 64;  // per-wave reduction rows of nwb waves
-  a.os_off = a.stg_off + (2 * 64 * g > 2048 ? round4(2 * 64 * g) : 2048);
-  total = a.os_off + 64 * OST;
+  a.red_off = a.aux_off + (bwd ? 2 * round4(TR * a.auxst) : 0);  // dF tile + Y tile
+  const int np = 64 * nwb < 512 ? 64 * nwb : 512;       // prologue owners (scratch: 2 np slots)
+  const int gp16 = (g + 15) / 16 * 16, dp16 = (a.dxw + 15) / 16 * 16;
+  const int rows = nwb * TR * (bwd ? dp16 : gp16);
+  a.stg_off = a.red_off + round4(rows > 2 * np ? rows : 2 * np);
+  if (bwd && dphi) {  // backward: the workgroup's 64-feature block of W_l ([2][64*g]), Omega_l ([64][OST])
+    a.os_off = a.stg_off + (2 * 64 * g > 2048 ? round4(2 * 64 * g) : 2048);
+    total = a.os_off + 64 * OST;
+  } else {
+    a.os_off = a.stg_off;
+    total = a.stg_off;
+  }
 }
 
 // floor(i / n) = (i * magic(n)) >> 20 for 0 <= i < 4096, 1 <= n <= 256
@@ -468,7 +484,7 @@ inline LayerK make_layer_k(const dgprf_plan_t& pl, const StepDev& sd, int l, int
   a.last = l == pl.n_layers - 1;
   a.likelihood = pl.likelihood;
   a.layer = l;
-  step_lds(a.d, a.g, a, lds_floats, nwb);
+  step_lds(a, lds_floats, nwb, bwd, sd.full_bayes || a.dxw > 0);
   // element-owner prologue: X tile + dF tile <= 512 elements, W/Omega block staged by float4
   const int dpad = round4(a.d);
   a.ws = sd.ws;
@@ -514,7 +530,50 @@ inline LayerK make_layer_k(const dgprf_plan_t& pl, const StepDev& sd, int l, int
   if (sd.full_bayes) lds_floats += NW * round4(2 * a.d + 1);
   a.main_blocks = 8 * a.rt_per_xcd * a.ns;
   a.pad_m = 0;
+  a.rt_per_rg = 1;
+  a.ncw = a.nrw = a.rg_fast = a.gred_off = a.rg_nit = 0;
   return a;
+}
+
+// Row-group backward layout of layer l (floats; xs at 0): false when the layer does not fit it
+// (more than 32 chunks per slice, or LDS past 160 KiB).  Shared by dgprf_plan_init (which enables
+// the row-group path only when every layer fits) and the launcher.
+struct RgCfg {
+  int ncw, nrw, nit, fast, aux, red, wsa, osa, ost, hred, gred, total;
+};
+inline bool rg_config(const dgprf_plan_t& pl, int l, bool fb, RgCfg& c) {
+  const int d = pl.d[l], g = pl.n_gp[l], cpw = pl.cpw[l];
+  const int dxw = l > 0 ? pl.n_gp[l - 1] : 0;
+  const bool rbf = pl.kind[l] == DGPRF_RBF, g1 = g == 1;
+  const int NOT = (g + 15) >> 4, CH = 4 * cpw;
+  if (CH > 32) return false;
+  int ncw = 16;
+  while (ncw > CH && ncw > 4) ncw >>= 1;  // largest power of two <= CH
+  if (NOT > 2) ncw = 16;                  // wide outputs: no row-waves (their gW sum in LDS)
+  c.ncw = ncw;
+  c.nrw = 16 / ncw;
+  c.nit = (CH + ncw - 1) / ncw;
+  if (c.nit > 2) return false;
+  const int rows = TR * c.nrw, xst = round4(d) + 1, auxst = g + 1;
+  const bool need_x = !(l == 0 && pl.d[0] > 32) || fb;  // layer 0 with A_1 precomputed: no X
+  int off = need_x ? round4(rows * xst) : 0;
+  c.aux = off;
+  off += 2 * round4(rows * auxst);
+  c.red = off;
+  if (dxw > 0) off += 16 * TR * ((dxw + 15) / 16 * 16);
+  const int nf = 64 * cpw;
+  c.wsa = off;
+  if (fb || dxw > 0) off += round4((rbf ? 2 : 1) * nf * g);
+  c.ost = nf + 4;
+  c.osa = off;
+  off += round4(dxw * c.ost);
+  c.hred = off;
+  if (fb) off += 16 * round4(2 * d + 1);
+  c.gred = off;
+  if (c.nrw > 1) off += 16 * (g1 ? c.nit * 2 * 64 : c.nit * NOT * 2 * 256);
+  c.total = off;
+  c.fast = ((need_x ? rows * round4(d) : 0) + rows * g <= 1024 && pl.ws_chain < (1 << 29)) ? 1 : 0;
+  return (int64_t)c.total * 4 <= 160 * 1024;
 }
 
 // Kernel launch dispatch of the forward / backward over (NOT, G1, RBF, waves) for one A-tile k-step
@@ -525,5 +584,8 @@ void k_step_fwd_launch2(int g, bool rbf, int nw, dim3 grid, size_t lds, hipStrea
 template <int KS>
 void k_step_bwd_launch2(int g, bool rbf, bool fb, bool w8, dim3 grid, size_t lds, hipStream_t s,
                         const LayerK& a);
+template <int KS>
+void k_step_bwd_rg_launch2(int g, bool rbf, bool fb, int nit, dim3 grid, size_t lds, hipStream_t s,
+                           const LayerK& a);
 
 }  // namespace dgprf_sk

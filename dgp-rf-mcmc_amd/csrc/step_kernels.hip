@@ -649,6 +649,37 @@ hipError_t launch_step_fwd(const dgprf_plan_t& pl, const StepDev& sd, int layer,
 }
 
 hipError_t launch_step_bwd(const dgprf_plan_t& pl, const StepDev& sd, int layer, hipStream_t s) {
+  if (pl.rt_per_group > 1) {  // row-group backward: at most 16 gW partial rows whatever B
+    RgCfg c;
+    if (!rg_config(pl, layer, sd.full_bayes != 0, c)) return hipErrorInvalidValue;
+    int lds_floats = 0;
+    LayerK a = make_layer_k(pl, sd, layer, lds_floats, /*bwd=*/true, 4);
+    a.n_rt = pl.n_gw_rows;
+    a.rt_per_xcd = (pl.n_gw_rows + 7) / 8;
+    a.main_blocks = 8 * a.rt_per_xcd * a.ns;
+    a.rt_per_rg = pl.rt_per_group;
+    a.ncw = c.ncw;
+    a.nrw = c.nrw;
+    a.rg_nit = c.nit;
+    a.rg_fast = c.fast;
+    a.aux_off = c.aux;
+    a.red_off = c.red;
+    a.wsa_off = c.wsa;
+    a.osa_off = c.osa;
+    a.osa_st = c.ost;
+    a.hred_off = c.hred;
+    a.gred_off = c.gred;
+    dim3 grid(a.main_blocks, 1, pl.n_chains);
+    const int d = pl.d[layer], g = pl.n_gp[layer];
+    const bool rbf = pl.kind[layer] == DGPRF_RBF, fb = sd.full_bayes != 0;
+    const size_t lds = (size_t)c.total * sizeof(float);
+    if (d <= 4) k_step_bwd_rg_launch2<1>(g, rbf, fb, c.nit, grid, lds, s, a);
+    else if (d <= 8) k_step_bwd_rg_launch2<2>(g, rbf, fb, c.nit, grid, lds, s, a);
+    else if (d <= 16) k_step_bwd_rg_launch2<4>(g, rbf, fb, c.nit, grid, lds, s, a);
+    else if (d <= 32) k_step_bwd_rg_launch2<8>(g, rbf, fb, c.nit, grid, lds, s, a);
+    else k_step_bwd_rg_launch2<0>(g, rbf, fb, c.nit, grid, lds, s, a);
+    return hipGetLastError();
+  }
   // 8 waves per workgroup for W-only steps whose slices are staged whole (a.wstage)
   bool w8 = !sd.full_bayes && pl.cpw[layer] % 4 == 0;
   int lds_floats = 0;
@@ -675,7 +706,7 @@ hipError_t launch_step_update(const dgprf_plan_t& pl, const StepDev& sd, const U
   a.mass = sd.mass;
   a.step = sd.step;
   a.w_total = (int32_t)pl.w_total;
-  a.n_rt = pl.n_row_tiles;
+  a.n_rt = pl.n_gw_rows;  // gW partial rows (one per row tile, or per row group)
   a.n_rt_pad = pl.n_rt_pad;
   a.n_layers = pl.n_layers;
   for (int l = 0; l < DGPRF_MAX_LAYERS; ++l) {

@@ -45,7 +45,8 @@ class Plan(ctypes.Structure):
         ("fwd_path", _i32), ("agemm_chunk_rows", _i32), ("fresh_z", _i32),
         ("initialised", _i32),
         ("d", _i32 * _L), ("P", _i32 * _L), ("ns", _i32 * _L), ("cpw", _i32 * _L),
-        ("n_row_tiles", _i32), ("n_rt_pad", _i32),
+        ("n_row_tiles", _i32), ("n_rt_pad", _i32), ("rt_per_group", _i32), ("n_gw_rows", _i32),
+        ("rg_full_bayes", _i32), ("pad1", _i32),
         ("omega_off", _i64 * _L), ("w_off", _i64 * _L), ("lis_off", _i64 * _L),
         ("mean_off", _i64 * _L), ("fp_off", _i64 * _L), ("dxp_off", _i64 * _L),
         ("gwp_off", _i64), ("logp_off", _i64),

@@ -133,14 +133,25 @@ typedef struct dgprf_plan {
   int32_t ns[DGPRF_MAX_LAYERS];     /* feature slices per step kernel */
   int32_t cpw[DGPRF_MAX_LAYERS];    /* 16-feature chunks per wave per slice */
   int32_t n_row_tiles;              /* ceil(B/16) */
-  int32_t n_rt_pad;                 /* n_row_tiles rounded up to 16 (zero rows in gW partials) */
+  int32_t n_rt_pad;                 /* n_gw_rows rounded up to 16 (zero rows in gW partials) */
+  int32_t rt_per_group;             /* row tiles per backward workgroup: 1 while B <= 256 (one gW
+                                       partial row per row tile), ceil(n_row_tiles / 16) beyond, so
+                                       the gW partials stay <= 16 rows whatever B (row-group
+                                       backward; 1 also when some layer does not fit it)        */
+  int32_t n_gw_rows;                /* gW partial rows: ceil(n_row_tiles / rt_per_group) <= 16
+                                       (or n_row_tiles when rt_per_group == 1)                  */
+  int32_t rg_full_bayes;            /* rt_per_group > 1: every layer also fits the full-Bayes
+                                       row-group backward (else full_bayes steps / gradients
+                                       return DGPRF_E_SHAPE for this batch size)                */
+  int32_t pad1;
   int64_t omega_off[DGPRF_MAX_LAYERS];
   int64_t w_off[DGPRF_MAX_LAYERS];
   int64_t lis_off[DGPRF_MAX_LAYERS];
   int64_t mean_off[DGPRF_MAX_LAYERS];
   int64_t fp_off[DGPRF_MAX_LAYERS];  /* F partials  [16][B][g] (per chain; slices >= ns stay 0) */
   int64_t dxp_off[DGPRF_MAX_LAYERS]; /* dX partials [16][B][g_{l-1}] (per chain, l>=1)      */
-  int64_t gwp_off;                   /* gW partials [n_rt_pad][w_total] (per chain)           */
+  int64_t gwp_off;                   /* gW partials [n_rt_pad][w_total] (per chain; rows past
+                                        n_gw_rows stay zero)                                    */
   int64_t logp_off;                  /* per-row minibatch log p [B] (per chain) */
   int64_t omega_total;
   int64_t w_total;

@@ -90,3 +90,14 @@ def test_entry_points_validate_before_enqueue():
     assert lib.dgprf_rf_features(7, None, 0, 1, None, 1, None, None, None) == N.E_ARG
     assert lib.dgprf_philox_normal(None, 4, 0, 0, 1, None) == N.E_ARG
     assert lib.dgprf_error_string(N.E_SHAPE) == b"unsupported shape"
+
+
+def test_row_group_workspace_bounded():
+    """gW partials never exceed 16 rows: workspace for B = 65,536 at config 2's shape holds
+    16 x w_total gW floats (host-only plan check, runs without a GPU)."""
+    from dgprf import _native as N
+    for B, rows in ((200, 13), (256, 16), (257, 9), (1024, 16), (8192, 16), (65536, 16)):
+        pl = N.make_plan(8, 1, [N.RBF] * 3, [1024] * 3, [8, 8, 1], False, N.LIK_GAUSSIAN, B, 1)
+        assert pl.n_gw_rows == rows, (B, pl.n_gw_rows)
+        assert pl.n_rt_pad == 16
+        assert (pl.rt_per_group > 1) == (B > 256)

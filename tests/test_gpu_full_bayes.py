@@ -322,6 +322,27 @@ def test_full_bayes_engine_grad_flags_and_scalar_lengthscale(dev, case):
 
 
 @pytest.mark.parametrize("case", [0, 1])
+def test_full_bayes_row_group_grad(dev, case):
+    """B = 600 (38 row tiles): the full-Bayes row-group backward keeps the hyper-parameter partials
+    per row group (<= 16 rows) like gW; every gradient against the oracle."""
+    spec_args, ard, flags = ENGINE_CASES[case]
+    rng = np.random.default_rng(300 + case)
+    eng = engine_for(spec_args, ard, flags)
+    p = random_params(rng, spec_args, ard)
+    load_chain(eng, p, 0)
+    B, N_ = 600, 5000
+    pl = eng.plan_ws(B)[0]
+    assert pl.rt_per_group == 3 and pl.n_gw_rows == 13 and pl.rg_full_bayes == 1
+    X = rng.standard_normal((B, spec_args[0]))
+    Y = rng.standard_normal((B, spec_args[1])) if spec_args[6] == "gaussian" else \
+        rng.integers(0, spec_args[1], (B, 1)).astype(float)
+    tr = O.Trainable(kernel="kernel" in flags, lik="lik" in flags, mean="mean" in flags,
+                     ard=[bool(a) for a in ard])
+    G = eng.grad(X, Y, N_, full_bayes=True)
+    check_grad(eng, G, 0, O.grad_full(p, X, Y, N_, tr), tr)
+
+
+@pytest.mark.parametrize("case", [0, 1])
 def test_full_bayes_engine_step_scalar_lengthscale(dev, case):
     """One step with injected noise; scalar length scales stay broadcast over their d slots."""
     spec_args, ard, flags = ENGINE_CASES[case]
