@@ -3,6 +3,7 @@
 // Host-side validation and planning mirror the reference's constructor and assertions
 // (models/dgp.py:34-52, 74-115; kernels/RBF.py:19-27; kernels/arc_cosine.py:13-16): configuration
 // errors are reported as return codes before anything is enqueued.
+#include <cstdlib>
 #include <cstring>
 #include <new>
 
@@ -115,7 +116,11 @@ hipError_t enqueue_step(const dgprf_plan_t& pl, const StepDev& sd, const UpdateD
   if (prep_gather) e = dgprf::launch_gather(pl, sd, s);
   // random_fixed=False layers: this step's Omega from fresh z (layers/rf_layers.py:39-41)
   if (e == hipSuccess && pl.fresh_z) e = dgprf::launch_fresh_omega(pl, sd, s);
-  for (int l = 0; l < pl.n_layers && e == hipSuccess; ++l) e = dgprf::launch_step_fwd(pl, sd, l, s);
+  if (dgprf_sk::step_fused_fwd(pl)) {  // large B, one chain: one all-layer forward launch
+    if (e == hipSuccess) e = dgprf::launch_step_fwd_fused(pl, sd, s);
+  } else {
+    for (int l = 0; l < pl.n_layers && e == hipSuccess; ++l) e = dgprf::launch_step_fwd(pl, sd, l, s);
+  }
   for (int l = pl.n_layers - 1; l >= 0 && e == hipSuccess; --l)
     e = dgprf::launch_step_bwd(pl, sd, l, s);
   if (e == hipSuccess) e = dgprf::launch_step_update(pl, sd, ud, nullptr, s, gather_next);
@@ -353,7 +358,8 @@ int dgprf_graph_create_sghmc(dgprf_graph_handle* out, const dgprf_plan_t* plan,
   if (step->full_bayes && plan->fresh_z) return DGPRF_E_ARG;
   hipStream_t cs;
   if (hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess) return DGPRF_E_HIP;
-  if (plan->a0_off >= 0) {  // library GEMM state (handle, tuned algorithm) before capture
+  if (plan->a0_off >= 0 && getenv("DGPRF_AGEMM") && getenv("DGPRF_AGEMM")[0] == 'l') {
+    // hipBLASLt comparison arm only: library GEMM state (handle, tuned algorithm) before capture
     // The warm-up writes the workspace's A_1 on `cs`, which is not ordered after the caller's
     // stream: let every earlier kernel (e.g. gradients still reading A_1) finish first.
     const StepDev sd0 = make_step_dev(*plan, *chain, *batch, step->step_offset);
@@ -434,7 +440,9 @@ int dgprf_profile_step(const dgprf_plan_t* plan, const dgprf_chain_t* chain,
       const int kk = j < L ? j : (j < 2 * L ? L + (2 * L - 1 - j) : 2 * L);
       e = hipEventRecord(ev[2 * kk], s);
       if (e != hipSuccess) break;
-      if (kk < L) e = dgprf::launch_step_fwd(*plan, sd, kk, s);
+      if (kk < L && dgprf_sk::step_fused_fwd(*plan))  // one all-layer forward (timed as layer 0)
+        e = kk == 0 ? dgprf::launch_step_fwd_fused(*plan, sd, s) : hipSuccess;
+      else if (kk < L) e = dgprf::launch_step_fwd(*plan, sd, kk, s);
       else if (kk < 2 * L) e = dgprf::launch_step_bwd(*plan, sd, kk - L, s);
       else e = dgprf::launch_step_update(*plan, sd, ud, nullptr, s);
       if (e == hipSuccess) e = hipEventRecord(ev[2 * kk + 1], s);

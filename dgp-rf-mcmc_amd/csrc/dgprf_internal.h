@@ -38,7 +38,9 @@ struct UpdateDev {
 };
 
 // In-kernel timestamps for a separate diagnostic build (-DDGPRF_STAMPS); never in the product.
-#ifdef DGPRF_STAMPS
+// The stamp array lives in the translation unit that defines DGPRF_STAMPS_TU (step_kernels.hip:
+// the update kernel); the other units' stamps compile to nothing (no -fgpu-rdc across units).
+#if defined(DGPRF_STAMPS) && defined(DGPRF_STAMPS_TU)
 extern __device__ unsigned long long g_dgprf_stamps[];
 #define DGPRF_STAMP_SLOTS 16
 #define DGPRF_STAMP_BASES (17 * 4096)
@@ -87,6 +89,9 @@ inline void set_lds_limit(const void* fn, size_t bytes) {
 // Forward / backward of one layer of the step (k_step_fwd / k_step_bwd).
 hipError_t launch_step_fwd(const dgprf_plan_t& pl, const StepDev& sd, int layer, hipStream_t s);
 hipError_t launch_step_bwd(const dgprf_plan_t& pl, const StepDev& sd, int layer, hipStream_t s);
+// Large minibatches, one chain (dgprf_sk::step_fused_fwd): the forward of every layer as one
+// launch of the predictive kernel, complete F_l into slice 0 of the F partial buffers.
+hipError_t launch_step_fwd_fused(const dgprf_plan_t& pl, const StepDev& sd, hipStream_t s);
 // Sums the gW partials, adds the prior term and applies the SGHMC update (or writes the gradient);
 // gather_next: extra workgroups gather step t+1's minibatch rows.
 hipError_t launch_step_update(const dgprf_plan_t& pl, const StepDev& sd, const UpdateDev& ud,
@@ -103,6 +108,12 @@ hipError_t launch_advance(int64_t* step, int64_t by, hipStream_t s);
 // The step's A_1 GEMM alone (plan.a0_off >= 0); dgprf_graph_create_sghmc runs it once before
 // capture so the GEMM's library handle and algorithm exist when the step is captured.
 hipError_t launch_step_agemm(const dgprf_plan_t& pl, const StepDev& sd, hipStream_t s);
+// The hand-written MFMA A_1 GEMM (agemm.hip): A[n_out][R] = X[n][d] Omega[d][R] (rows >= n
+// zero) for `batch` chains (element strides sx, so, sa; so = 0: shared Omega).  false: shape
+// outside the kernel (d, ldx, R not multiples of 4, or too large for 32-bit offsets).
+bool own_agemm(const float* X, int64_t n, int64_t n_out, int ldx, int d, const float* om, int R,
+               float* aout, int batch, int64_t sx, int64_t so, int64_t sa, hipStream_t s,
+               hipError_t* err);
 // hipBLASLt fp32 A = X Omega (row-major, A row stride R) for `batch` chains (element strides sx,
 // so, sa; so = 0: shared Omega).  false: no library path for the shape (caller uses its kernel).
 bool blas_agemm(const float* X, int64_t n, int ldx, int d, const float* om, int R, float* aout,

@@ -24,6 +24,24 @@ namespace dgprf_sk {
 
 constexpr int RG_WAVES = 16;
 
+// In-kernel timestamps of the diagnostic -DDGPRF_STAMPS build only (into the buffer the launcher
+// passes in a.stamps; never in the product).
+#ifdef DGPRF_STAMPS
+#define RG_STAMP(base, i)                                                        \
+  do {                                                                           \
+    if (threadIdx.x == 0 && a.stamps) {                                          \
+      __builtin_amdgcn_sched_barrier(0);                                         \
+      a.stamps[(size_t)(base) * 16 + (i)] = __builtin_amdgcn_s_memtime();        \
+      __builtin_amdgcn_sched_barrier(0);                                         \
+    }                                                                            \
+  } while (0)
+#else
+#define RG_STAMP(base, i) \
+  do {                    \
+    (void)(base);         \
+  } while (0)
+#endif
+
 // One prologue element of a super tile (rows row0 .. row0 + rows, valid below row_end): X tile
 // elements first (rows x dpad, only when need_x), then dF tile elements (rows x g) with their Y.
 __device__ __forceinline__ void rg_issue(const LayerK& a, int chain, int row0, int row_end, int rows,
@@ -42,9 +60,11 @@ __device__ __forceinline__ void rg_issue(const LayerK& a, int chain, int row0, i
   const int w = isx ? a.gp : a.g;
   const int base = (isx ? a.fprev_off : a.dsrc_off) + b * w + c;
   const int str = a.B * w;
+  // complete sources (fused forward: F_{l-1}, and F_L for the last layer) hold slice 0 only
+  const int nsl = (a.cmp && (isx || a.last)) ? 1 : NSM;
 #pragma unroll
   for (int sl = 0; sl < NSM; ++sl)
-    e.v[sl] = bload1(rws, fromp ? (uint32_t)((base + sl * str) * 4) : DGPRF_OOB);
+    e.v[sl] = bload1(rws, fromp && sl < nsl ? (uint32_t)((base + sl * str) * 4) : DGPRF_OOB);
   const bool xdat = inb && isx && c >= a.gp && c < a.d;
   e.xd = bload1(rx, xdat ? (uint32_t)((b * ndat + (c - a.gp)) * 4) : DGPRF_OOB);
   const int yc = a.likelihood == DGPRF_LIK_GAUSSIAN ? a.g : 1;
@@ -80,7 +100,8 @@ __device__ __forceinline__ void rg_load_generic(const LayerK& a, int chain, int 
       const int bc = min(b, a.B - 1), kc = min(k, a.d - 1);
       float v;
       if (kc < a.gp)
-        v = sum_slices(fprev + (int64_t)bc * a.gp + kc, (int64_t)a.B * a.gp);
+        v = a.cmp ? fprev[(int64_t)bc * a.gp + kc]
+                  : sum_slices(fprev + (int64_t)bc * a.gp + kc, (int64_t)a.B * a.gp);
       else
         v = xr[(int64_t)bc * a.d_in + (kc - a.gp)];
       xs[r * a.xst + k] = (b < row_end && k < a.d) ? v : 0.f;
@@ -90,7 +111,8 @@ __device__ __forceinline__ void rg_load_generic(const LayerK& a, int chain, int 
   const int g = a.g, yc = a.likelihood == DGPRF_LIK_GAUSSIAN ? g : 1;
   for (int e = threadIdx.x; e < rows * g; e += blockDim.x) {
     const int r = e / g, o = e - r * g, b = row0 + r, bc = min(b, a.B - 1);
-    const float v = sum_slices(src + (int64_t)bc * g + o, (int64_t)a.B * g);
+    const float v = (a.cmp && a.last) ? src[(int64_t)bc * g + o]
+                                      : sum_slices(src + (int64_t)bc * g + o, (int64_t)a.B * g);
     dfs[r * a.auxst + o] = b < row_end ? v : 0.f;
     if (a.last) ysh[r * a.auxst + o] = yr[(int64_t)bc * a.y_cols + min(o, yc - 1)];
   }
@@ -102,6 +124,8 @@ __global__ __launch_bounds__(64 * RG_WAVES) void k_step_bwd_rg(const LayerK a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   int rg, sl;
   if (!tile_of_block(a, rg, sl)) return;
+  const int stamp_base = (a.layer * 2 + 1) * 4096 + blockIdx.z * gridDim.x + blockIdx.x;
+  RG_STAMP(stamp_base, 0);
   const int chain = blockIdx.z;
   const float* __restrict__ om = a.om + (int64_t)chain * a.om_cs;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, lr = lane & 15, lq = lane >> 4;
@@ -194,7 +218,8 @@ __global__ __launch_bounds__(64 * RG_WAVES) void k_step_bwd_rg(const LayerK a) {
   const int wave0 = __builtin_amdgcn_readfirstlane(t & ~63);
   Elem e0;  // one prologue element per thread (rg_fast: total <= 1024)
   e0.dst = -1;
-  if (a.rg_fast && wave0 < total) rg_issue(a, chain, rt0 * TR, row_end, rows, nx, t, e0);
+  if (a.rg_fast && wave0 < total && !(a.dbg & 1)) rg_issue(a, chain, rt0 * TR, row_end, rows, nx, t, e0);
+  RG_STAMP(stamp_base, 1);
   float* dxp = a.dxout + (int64_t)chain * a.ws_cs + (int64_t)sl * B * dxw;
   const float* a0b = KS == 0 && a.a0 ? a.a0 + (int64_t)chain * a.ws_cs : nullptr;
 
@@ -206,6 +231,7 @@ __global__ __launch_bounds__(64 * RG_WAVES) void k_step_bwd_rg(const LayerK a) {
       rg_load_generic(a, chain, row0, row_end, rows, need_x, xs, dfs, ysh);
     }
     __syncthreads();
+    if (it == 0) RG_STAMP(stamp_base, 2);
     if (a.last) {
       // likelihood gradient dF = -(1/B) dlogp/dF (likelihoods/gaussian.py:18-25, softmax.py:8-15)
       float lvrow = 0.f;
@@ -255,7 +281,7 @@ __global__ __launch_bounds__(64 * RG_WAVES) void k_step_bwd_rg(const LayerK a) {
     }
     // next super tile's partial sums: loads in flight while this one computes
     if (a.rg_fast && it + 1 < n_iter && wave0 < total)
-      rg_issue(a, chain, row0 + rows, row_end, rows, nx, t, e0);
+      if (!(a.dbg & 1)) rg_issue(a, chain, row0 + rows, row_end, rows, nx, t, e0);
     // ---- this wave's row tile rw of the super tile
     const float* xw = xs + rw * TR * a.xst;
     const float* dw = dfs + rw * TR * a.auxst;
@@ -286,7 +312,7 @@ __global__ __launch_bounds__(64 * RG_WAVES) void k_step_bwd_rg(const LayerK a) {
     f4 dxa[4] = {f4zero(), f4zero(), f4zero(), f4zero()};
 #pragma unroll
     for (int i = 0; i < NIT; ++i) {
-      if (!live || !chunk_ok(i)) continue;  // wave-uniform
+      if (!live || !chunk_ok(i) || (a.dbg & 2)) continue;  // wave-uniform
       const int ci = i * ncw + cw, f0 = chunk_f0(i);
       const float* wsc = wsa + ci * 16 * g;
       const int whalf = nf * g;
@@ -418,8 +444,9 @@ __global__ __launch_bounds__(64 * RG_WAVES) void k_step_bwd_rg(const LayerK a) {
         }
       }
     }
+    if (it == 0) RG_STAMP(stamp_base, 3);
     // ---- dX of the super tile: the chunk-waves' tiles summed in LDS, stored as the slice partial
-    if (dxw > 0) {
+    if (dxw > 0 && !(a.dbg & 4)) {
       float* redw = red + wave * TR * DP;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt)
@@ -439,7 +466,10 @@ __global__ __launch_bounds__(64 * RG_WAVES) void k_step_bwd_rg(const LayerK a) {
       }
     }
     __syncthreads();  // LDS tiles free for the next super tile
+    if (it == 0) RG_STAMP(stamp_base, 4);
+    if (it == 1) RG_STAMP(stamp_base, 5);
   }
+  RG_STAMP(stamp_base, 6);
 
   // ---- the group's gW partial row: row-waves summed in order (LDS), then stored
   float* gwp = a.gwp + (int64_t)chain * a.ws_cs + (int64_t)rg * a.w_cs;
@@ -509,6 +539,7 @@ __global__ __launch_bounds__(64 * RG_WAVES) void k_step_bwd_rg(const LayerK a) {
       }
     }
   }
+  RG_STAMP(stamp_base, 7);
   if (FB) {
     // log_amp term over the wave, then the workgroup's partial row [2d+1] in wave order
     float v = sum16(ampl);
@@ -526,6 +557,10 @@ __global__ __launch_bounds__(64 * RG_WAVES) void k_step_bwd_rg(const LayerK a) {
     if (a.last && a.lik_fb && threadIdx.x == 0 && sl == 0)
       a.hpl[(int64_t)chain * a.ws_cs + rg] = lvacc;
   }
+#ifdef DGPRF_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  RG_STAMP(stamp_base, 14);
 }
 
 // launch dispatch: NOT x G1 x RBF x FB x NIT for one KS

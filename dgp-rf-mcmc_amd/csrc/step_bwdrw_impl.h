@@ -1,0 +1,479 @@
+// step_bwdrw_impl.h — the row-wave step backward k_step_bwd_rw, included by step_bwdrw_k<KS>.hip.
+//
+// The row-group backward (step_bwdrg_impl.h) for narrow slices (at most 8 accumulator tiles of gW
+// per slice: config 2's RBF n_rf 1024 / g 8, config 3's ARC n_rf 2048 / g 9) after the fused
+// all-layer forward (complete F_l, plan rt_per_group >= 8): every wave of an 8-wave workgroup owns
+// the WHOLE feature slice for its own row tiles (rt0 + w, rt0 + w + 8, ...), so
+//   * a wave's dX rows are complete slice sums in its own registers — stored straight to the slice
+//     partial, no cross-wave LDS reduction;
+//   * its X / dF tiles live in a wave-private LDS region (the next tile's partial sums prefetched
+//     into registers while the current one computes);
+//   * nothing in the row-tile loop waits for another wave: no workgroup barrier until the end,
+//     where the 8 waves' gW accumulators are summed in LDS in wave order and the group's gW
+//     partial row is written (one row per group, <= 16 whatever B, as in the row-group kernel).
+// Same arithmetic as k_step_bwd (analytic tape.gradient, models/dgp.py:194-198).  Deterministic:
+// fixed row-tile order inside each wave's accumulators, then waves 0..7.
+#pragma once
+#include "step_common.h"
+
+namespace dgprf_sk {
+
+constexpr int RW_WAVES = 8;
+
+// NCH: 16-feature chunks of the slice (4 cpw); EX / ED: prefetched X / dF elements per lane
+// (16 dpad / 64, 16 g / 64 rounded up).
+template <int KS, int NOT, bool RBF, bool G1, bool FB, int NCH, int ED>
+__global__ __launch_bounds__(64 * RW_WAVES) void k_step_bwd_rw(const LayerK a) {
+  constexpr int EX = KS;  // 16 rows x 4 KS columns of X = KS elements per lane
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  int rg, sl;
+  if (!tile_of_block(a, rg, sl)) return;
+  const int chain = blockIdx.z;
+  const float* __restrict__ om = a.om + (int64_t)chain * a.om_cs;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, lr = lane & 15, lq = lane >> 4;
+  const int R = a.R, g = a.g, d = a.d, B = a.B, dxw = a.dxw;
+  const int nf = 64 * a.cpw, fb0 = sl * nf;
+  const int n_rt_all = (B + TR - 1) / TR;
+  const int rt0 = rg * a.rt_per_rg;
+  const int rt_end = min(rt0 + a.rt_per_rg, n_rt_all);
+  const int row_end = min(rt_end * TR, B);
+  constexpr int KGM = 4 * NOT;
+  const int ND = (dxw + 15) >> 4;
+  const bool dphi = FB || dxw > 0;
+  const int xst = a.xst, dst = a.auxst;
+  float* wsa = smem + a.wsa_off;               // [RBF ? 2 : 1][nf][g]
+  float* osa = smem + a.osa_off;               // [max(d, dxw)][osa_st]
+  float* xw = smem + a.aux_off + wave * a.red_off;  // wave-private: X [16][xst], dF, Y [16][dst]
+  float* dw = xw + round4(TR * xst);
+  float* yw = dw + round4(TR * dst);
+  const float cl = a.cptr[(int64_t)chain * a.der_cs];
+
+  // ---- the slice's W rows (both halves) and Omega rows k < max(d, dxw), once (zero past R)
+  {
+    const float* W = a.W + (int64_t)chain * a.w_cs;
+    const int nh = RBF ? 2 : 1, nwf = nf * g;
+    if (dphi) {
+      if (((int64_t)R * g) % 4 == 0) {
+        const int n4 = nwf / 4;
+        for (int e = threadIdx.x; e < nh * n4; e += blockDim.x) {
+          const int h = e >= n4, e2 = 4 * (e - h * n4);
+          f4 v = f4zero();
+          if (fb0 + (e2 + 3) / g < R) v = *reinterpret_cast<const f4*>(W + ((int64_t)h * R + fb0) * g + e2);
+          *reinterpret_cast<f4*>(wsa + h * nwf + e2) = v;
+        }
+      } else {
+        for (int e = threadIdx.x; e < nh * nwf; e += blockDim.x) {
+          const int h = e >= nwf, e2 = e - h * nwf;
+          wsa[e] = fb0 + e2 / g < R ? W[((int64_t)h * R + fb0) * g + e2] : 0.f;
+        }
+      }
+    }
+    const int orows = d > dxw ? d : dxw;
+    for (int e = threadIdx.x; e < orows * nf; e += blockDim.x) {
+      const int k = e / nf, c = e - k * nf;
+      osa[k * a.osa_st + c] = fb0 + c < R ? om[(int64_t)k * R + fb0 + c] : 0.f;
+    }
+  }
+  constexpr int NZ = (4 * KS + 15) / 16;
+  const rsrc_t rz = make_rsrc(a.z, FB ? (int64_t)d * R : 0);
+  f4 zpf[NCH][FB ? NZ : 1];
+  if (FB)
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int dt = 0; dt < NZ; ++dt) {
+        const int k = dt * 16 + lr, f0 = fb0 + c * 16;
+        zpf[c][dt] = bload4(rz, k < d && f0 + 4 * lq < R ? (uint32_t)(((int64_t)k * R + f0 + 4 * lq) * 4)
+                                                          : DGPRF_OOB);
+      }
+
+  f4 gacc[NCH][NOT][2];
+  float g1c[NCH], g1s[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    g1c[c] = g1s[c] = 0.f;
+#pragma unroll
+    for (int ot = 0; ot < NOT; ++ot) gacc[c][ot][0] = gacc[c][ot][1] = f4zero();
+  }
+  const int hst = round4(2 * d + 1);
+  float* hw = smem + a.hred_off + wave * hst;
+  float ampl = 0.f, lvacc = 0.f;
+  if (FB)
+    for (int e = lane; e < hst; e += 64) hw[e] = 0.f;
+
+  // ---- prefetch of one row tile: X (complete F_{l-1} | dataset columns; KS x 4 columns, lane
+  // owns column 4 ks + lq of row lr) and dF (16 slices of dX_{l+1}, or complete F_L; element
+  // u = lane + 64 e of the [16][g] tile)
+  const rsrc_t rws = make_rsrc(a.ws + (int64_t)chain * a.ws_cs, a.ws_cs);
+  const rsrc_t rxd = make_rsrc(a.xrows + (int64_t)chain * a.xrow_cs, (int64_t)B * (d - a.gp));
+  const rsrc_t ry = make_rsrc(a.yrows + (int64_t)chain * a.yrow_cs, (int64_t)B * a.y_cols);
+  const int nsl = a.last ? 1 : NSM;  // F_L complete (fused forward) / dX_{l+1} slice partials
+  const int yc = a.likelihood == DGPRF_LIK_GAUSSIAN ? g : 1;
+  float px[EX], pd[ED][NSM], py[ED];
+  auto issue = [&](int rt) {
+    const int row0 = rt * TR;
+#pragma unroll
+    for (int e = 0; e < EX; ++e) {
+      const int k = 4 * e + lq, b = row0 + lr;
+      const bool ok = b < row_end && k < d;
+      px[e] = k < a.gp ? bload1(rws, ok ? (uint32_t)((a.fprev_off + b * a.gp + k) * 4) : DGPRF_OOB)
+                       : bload1(rxd, ok ? (uint32_t)((b * (d - a.gp) + (k - a.gp)) * 4) : DGPRF_OOB);
+    }
+#pragma unroll
+    for (int e = 0; e < ED; ++e) {
+      const int u = lane + 64 * e, r = u / g, o = u - r * g, b = row0 + r;
+      const bool ok = u < TR * g && b < row_end;
+#pragma unroll
+      for (int s = 0; s < NSM; ++s)
+        pd[e][s] = bload1(rws, ok && s < nsl ? (uint32_t)((a.dsrc_off + s * B * g + b * g + o) * 4)
+                                              : DGPRF_OOB);
+      py[e] = bload1(ry, ok && a.last ? (uint32_t)((b * a.y_cols + min(o, yc - 1)) * 4) : DGPRF_OOB);
+    }
+  };
+  const int dpad = round4(d);  // the X tile row holds columns < dpad (xst = dpad + 1)
+  auto commit = [&]() {
+#pragma unroll
+    for (int e = 0; e < EX; ++e)
+      if (4 * e + lq < dpad) xw[lr * xst + 4 * e + lq] = px[e];
+#pragma unroll
+    for (int e = 0; e < ED; ++e) {
+      const int u = lane + 64 * e, r = u / g, o = u - r * g;
+      float v = pd[e][0];
+#pragma unroll
+      for (int s = 1; s < NSM; ++s) v += pd[e][s];
+      if (u < TR * g) {
+        dw[r * dst + o] = v;
+        yw[r * dst + o] = py[e];
+      }
+    }
+  };
+
+  float* dxp = a.dxout + (int64_t)chain * a.ws_cs + (int64_t)sl * B * dxw;
+  __syncthreads();  // staged slice visible to every wave
+  int rt = rt0 + wave;
+  if (rt < rt_end) issue(rt);
+  for (; rt < rt_end; rt += RW_WAVES) {
+    const int row0 = rt * TR;
+    commit();
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes done
+    __builtin_amdgcn_wave_barrier();
+    if (a.last) {
+      // likelihood gradient dF = -(1/B) dlogp/dF (likelihoods/gaussian.py:18-25, softmax.py:8-15)
+      float lvrow = 0.f;
+      if (lane < TR) {
+        const int b = row0 + lane;
+        float* df = dw + lane * dst;
+        if (b < row_end) {
+          const float* y = yw + lane * dst;
+          const float invB = 1.0f / (float)B;
+          float logp = 0.f;
+          if (a.likelihood == DGPRF_LIK_GAUSSIAN) {
+            const float var = a.varptr[(int64_t)chain * a.der_cs];
+            const float logvar = logf(var);
+            float lv = 0.f;
+            for (int o = 0; o < g; ++o) {
+              const float diff = y[o] - df[o];
+              logp += -0.5f * (LOG_2PI + logvar + diff * diff / var);
+              df[o] = -(diff / var) * invB;
+              lv += 0.5f * (1.f - diff * diff / var);
+            }
+            lvrow = lv * invB;
+          } else {
+            float mx = -INFINITY;
+            for (int o = 0; o < g; ++o) mx = fmaxf(mx, df[o]);
+            float se = 0.f;
+            for (int o = 0; o < g; ++o) se += expf(df[o] - mx);
+            const float lse = mx + logf(se);
+            const int label = (int)y[0];
+            const float bad = (label >= 0 && label < g) ? 0.f : __builtin_nanf("");
+            for (int o = 0; o < g; ++o) {
+              const float f = df[o];
+              if (o == label) logp = f - lse;
+              df[o] = (expf(f - lse) - (o == label ? 1.f : 0.f)) * invB + bad;
+            }
+            logp += bad;
+          }
+          if (sl == 0) a.logp[(int64_t)chain * a.ws_cs + b] = logp;
+        }
+      }
+      if (FB && a.lik_fb) lvacc += sum16(lvrow);
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+    }
+    // the next row tile's loads are in flight while this one computes
+    if (rt + RW_WAVES < rt_end) issue(rt + RW_WAVES);
+    float xf[8];
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) xf[ks] = (ks < KS && 4 * ks < d) ? xw[lr * xst + 4 * ks + lq] : 0.f;
+    float dff[KGM];
+#pragma unroll
+    for (int ks = 0; ks < KGM; ++ks) {
+      const int o = 4 * ks + lq;
+      dff[ks] = (o < g) ? dw[lr * dst + o] : 0.f;
+    }
+    float dfg[NOT][4];
+#pragma unroll
+    for (int ot = 0; ot < NOT; ++ot)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int o = ot * 16 + lr;
+        dfg[ot][r] = (o < g) ? dw[(4 * lq + r) * dst + o] : 0.f;
+      }
+    const int KG = (g + 3) >> 2;
+    const float dg1 = G1 ? dw[lr * dst] : 0.f;
+    float dg4[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dg4[r] = G1 ? dw[(4 * lq + r) * dst] : 0.f;
+    f4 dxa[2] = {f4zero(), f4zero()};
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int f0 = fb0 + c * 16;
+      if (f0 >= R) break;  // wave-uniform
+      const float* wsc = wsa + c * 16 * g;
+      const int whalf = nf * g;
+      const float* osc = osa + c * 16;
+      // Omega fragments of the A tile from the staged rows: omk[ks] = Omega[4 ks + lq][f0 + lr]
+      float omk[8];
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks)
+        omk[ks] = (ks < KS && 4 * ks + lq < d) ? osc[(4 * ks + lq) * a.osa_st + lr] : 0.f;
+      float wd0[KGM], wd1[KGM];
+      f4 oxv[4];
+      if (dphi) {
+        const bool frow = f0 + lr < R;
+#pragma unroll
+        for (int ks = 0; ks < KGM; ++ks) {
+          const int o = 4 * ks + lq, wo = lr * g + o;
+          const bool ok = o < g && frow;
+          wd0[ks] = G1 ? 0.f : (ok ? wsc[wo] : 0.f);
+          wd1[ks] = (G1 || !RBF) ? 0.f : (ok ? wsc[whalf + wo] : 0.f);
+        }
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+          oxv[dt] = dt < ND ? *reinterpret_cast<const f4*>(osc + (dt * 16 + lr) * a.osa_st + 4 * lq)
+                            : f4zero();
+      }
+      const f4 at_t = a_tile<KS, true>(om, R, d, f0, omk, xf, xw, xst, lr, lq);
+      f4 at_n = f4zero(), dpc = f4zero(), dps = f4zero();
+      if (dphi) {
+        at_n = a_tile<KS, false>(om, R, d, f0, omk, xf, xw, xst, lr, lq);
+        if (G1) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int fl = c * 16 + 4 * lq + r;
+            const bool ok = f0 + 4 * lq + r < R;
+            dpc[r] = ok ? dg1 * wsa[fl] : 0.f;
+            dps[r] = (ok && RBF) ? dg1 * wsa[whalf + fl] : 0.f;
+          }
+        } else {
+#pragma unroll
+          for (int ks = 0; ks < KGM; ++ks)
+            if (ks < KG) {
+              dpc = mfma16(wd0[ks], dff[ks], dpc);
+              if (RBF) dps = mfma16(wd1[ks], dff[ks], dps);
+            }
+        }
+      }
+      float q0[4], q1[4];
+      features<RBF>(at_t, cl, q0, q1);
+      float da[4];
+      if (dphi) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if (RBF) {
+            float sv, cv;
+            rf_sincos(at_n[r], &sv, &cv);
+            da[r] = -(cl * sv) * dpc[r] + (cl * cv) * dps[r];
+            if (FB) ampl += dpc[r] * (cl * cv) + dps[r] * (cl * sv);
+          } else {
+            da[r] = at_n[r] > 0.f ? cl * dpc[r] : 0.f;
+            if (FB) ampl += dpc[r] * (cl * fmaxf(at_n[r], 0.f));
+          }
+        }
+      }
+      if (G1) {
+        float gc = 0.f, gs = 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          gc = fmaf(q0[r], dg4[r], gc);
+          if (RBF) gs = fmaf(q1[r], dg4[r], gs);
+        }
+        gc += __shfl_xor(gc, 16);
+        gc += __shfl_xor(gc, 32);
+        if (RBF) {
+          gs += __shfl_xor(gs, 16);
+          gs += __shfl_xor(gs, 32);
+        }
+        g1c[c] += gc;
+        g1s[c] += gs;
+      } else {
+#pragma unroll
+        for (int ot = 0; ot < NOT; ++ot)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            gacc[c][ot][0] = mfma16(q0[r], dfg[ot][r], gacc[c][ot][0]);
+            if (RBF) gacc[c][ot][1] = mfma16(q1[r], dfg[ot][r], gacc[c][ot][1]);
+          }
+      }
+      if (dxw > 0) {
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+          if (dt < ND) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dxa[dt] = mfma16(oxv[dt][r], da[r], dxa[dt]);
+          }
+      }
+      if (FB) {
+        float rs = (da[0] + da[1]) + (da[2] + da[3]);
+        rs += __shfl_xor(rs, 16);
+        rs += __shfl_xor(rs, 32);
+#pragma unroll
+        for (int dt = 0; dt < NZ; ++dt) {
+          f4 dz = f4zero();
+#pragma unroll
+          for (int r = 0; r < 4; ++r) dz = mfma16(zpf[c][dt][r], da[r], dz);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int kk = dt * 16 + 4 * lq + r;
+            const float xv = kk < d ? xw[lr * xst + kk] : 0.f;
+            const float s1 = sum16(xv * dz[r]);
+            const float s2 = sum16(xv * rs);
+            if (lr == 0 && kk < d) {
+              hw[kk] += s1;
+              hw[d + kk] += s2;
+            }
+          }
+        }
+      }
+    }
+    // dX rows of this tile: the slice's complete sum (dxa[dt][r] = dX[row lr][dt 16 + 4 lq + r])
+    if (dxw > 0) {
+      const int b = row0 + lr;
+      if (b < row_end) {
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+          if (dt < ND) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int k = dt * 16 + 4 * lq + r;
+              if (k < dxw) dxp[(int64_t)b * dxw + k] = dxa[dt][r];
+            }
+          }
+      }
+    }
+  }
+
+  // ---- the group's gW partial row: the 8 waves' accumulators summed in wave order
+  __syncthreads();
+  constexpr int GSZ = G1 ? NCH * 2 * 64 : NCH * NOT * 2 * 256;
+  float* gred = smem + a.gred_off;
+  {
+    float* gw = gred + wave * GSZ;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      if (G1) {
+        gw[(c * 2) * 64 + lane] = g1c[c];
+        gw[(c * 2 + 1) * 64 + lane] = g1s[c];
+      } else {
+#pragma unroll
+        for (int ot = 0; ot < NOT; ++ot)
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+            *reinterpret_cast<f4*>(gw + ((c * NOT + ot) * 2 + h) * 256 + 4 * lane) = gacc[c][ot][h];
+      }
+    }
+  }
+  if (FB) {
+    float v = sum16(ampl);
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    if (lane == 0) {
+      hw[2 * d] = v;
+      hw[2 * d + 1] = lvacc;  // padding slot of the wave's row (hst >= 2 d + 2)
+    }
+  }
+  __syncthreads();
+  // every thread sums a strided share of the gW values in wave order and stores them
+  float* gwp = a.gwp + (int64_t)chain * a.ws_cs + (int64_t)rg * a.w_cs;
+  if (G1) {
+    for (int e = threadIdx.x; e < NCH * 2 * 16; e += blockDim.x) {
+      const int c = e / 32, h = (e / 16) & 1, fl = e & 15;  // lanes 0..15 hold features fl
+      float v = gred[(c * 2 + h) * 64 + fl];
+      for (int w = 1; w < RW_WAVES; ++w) v += gred[w * GSZ + (c * 2 + h) * 64 + fl];
+      const int f = fb0 + c * 16 + fl;
+      if (f < R && (h == 0 || RBF)) gwp[h * R + f] = v;
+    }
+  } else {
+    for (int e = threadIdx.x; e < NCH * NOT * 2 * 256; e += blockDim.x) {
+      // e = ((c NOT + ot) 2 + h) 256 + 4 lane + r: gacc[c][ot][h][r] of lane
+      const int blk = e >> 8, within = e & 255, ln = within >> 2, r = within & 3;
+      const int h = blk & 1, ot = (blk >> 1) % NOT, c = (blk >> 1) / NOT;
+      if (h == 1 && !RBF) continue;
+      float v = gred[e];
+      for (int w = 1; w < RW_WAVES; ++w) v += gred[w * GSZ + e];
+      // gacc[c][ot][h][r] of lane ln = gW[f0 + 4 (ln >> 4) + r][ot 16 + (ln & 15)] (half h)
+      const int f = fb0 + c * 16 + 4 * (ln >> 4) + r, o = ot * 16 + (ln & 15);
+      if (f < R && o < g) gwp[(int64_t)(h * R + f) * g + o] = v;
+    }
+  }
+  if (FB) {
+    float* hp = a.hp + (int64_t)chain * a.ws_cs + ((int64_t)rg * NSM + sl) * hst;
+    const float* h0 = smem + a.hred_off;
+    for (int e = threadIdx.x; e < 2 * d + 1; e += blockDim.x) {
+      float s = h0[e];
+      for (int w = 1; w < RW_WAVES; ++w) s += h0[w * hst + e];
+      hp[e] = s;
+    }
+    if (a.last && a.lik_fb && threadIdx.x == 0 && sl == 0) {
+      float s = h0[2 * d + 1];
+      for (int w = 1; w < RW_WAVES; ++w) s += h0[w * hst + 2 * d + 1];
+      a.hpl[(int64_t)chain * a.ws_cs + rg] = s;
+    }
+  }
+}
+
+template <int KS, int NOT, bool G1, int NCH, int ED>
+void k_step_bwd_rw_launch4(bool rbf, bool fb, dim3 grid, size_t lds, hipStream_t s, const LayerK& a) {
+#define DGPRF_BWDRW(R_, F_)                                                                       \
+  do {                                                                                           \
+    dgprf::set_lds_limit((const void*)k_step_bwd_rw<KS, NOT, R_, G1, F_, NCH, ED>, lds);        \
+    hipLaunchKernelGGL((k_step_bwd_rw<KS, NOT, R_, G1, F_, NCH, ED>), grid, dim3(64 * RW_WAVES),  \
+                       lds, s, a);                                                               \
+  } while (0)
+  if (rbf) {
+    if (fb) DGPRF_BWDRW(true, true);
+    else DGPRF_BWDRW(true, false);
+  } else {
+    if (fb) DGPRF_BWDRW(false, true);
+    else DGPRF_BWDRW(false, false);
+  }
+#undef DGPRF_BWDRW
+}
+// g <= 12 (ED = ceil(16 g / 64) <= 3), 4 or 8 chunks per slice
+template <int KS>
+void k_step_bwd_rw_launch2(int g, bool rbf, bool fb, int nch, dim3 grid, size_t lds,
+                           hipStream_t s, const LayerK& a) {
+  const int ed = (16 * g + 63) / 64;
+#define DGPRF_RW_ED(G1_, NCH_)                                                         \
+  do {                                                                                \
+    if (ed <= 1) k_step_bwd_rw_launch4<KS, 1, G1_, NCH_, 1>(rbf, fb, grid, lds, s, a); \
+    else if (ed == 2) k_step_bwd_rw_launch4<KS, 1, G1_, NCH_, 2>(rbf, fb, grid, lds, s, a); \
+    else k_step_bwd_rw_launch4<KS, 1, G1_, NCH_, 3>(rbf, fb, grid, lds, s, a);         \
+  } while (0)
+  if (g == 1) {
+    if (nch == 4) k_step_bwd_rw_launch4<KS, 1, true, 4, 1>(rbf, fb, grid, lds, s, a);
+    else k_step_bwd_rw_launch4<KS, 1, true, 8, 1>(rbf, fb, grid, lds, s, a);
+  } else if (nch == 4) {
+    DGPRF_RW_ED(false, 4);
+  } else {
+    DGPRF_RW_ED(false, 8);
+  }
+#undef DGPRF_RW_ED
+}
+
+}  // namespace dgprf_sk
+
+#ifdef DGPRF_KS
+template void dgprf_sk::k_step_bwd_rw_launch2<DGPRF_KS>(int, bool, bool, int, dim3, size_t,
+                                                        hipStream_t, const dgprf_sk::LayerK&);
+#endif

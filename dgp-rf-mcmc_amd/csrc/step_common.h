@@ -81,6 +81,10 @@ struct LayerK {
   // row-group backward (k_step_bwd_rg, minibatches of > 16 row tiles): rt_per_rg row tiles per
   // workgroup, ncw chunk-waves x nrw row-waves, register-prefetched prologue when rg_fast
   int32_t rt_per_rg, ncw, nrw, rg_fast, gred_off, rg_nit;
+  int32_t dbg;           // diagnostic switches (DGPRF_DBG env, never set in the product)
+  int32_t cmp;           // row-group backward after the fused forward (step_fused_fwd): every
+                         // F_l is complete in slice 0 of its partial buffer (one load, not 16)
+  unsigned long long* stamps;  // -DDGPRF_STAMPS diagnostic build: stamp buffer, else null
 };
 
 // Block -> (row tile, slice): blocks are dealt round-robin over the 8 XCDs, so block b's XCD group
@@ -532,6 +536,8 @@ inline LayerK make_layer_k(const dgprf_plan_t& pl, const StepDev& sd, int l, int
   a.pad_m = 0;
   a.rt_per_rg = 1;
   a.ncw = a.nrw = a.rg_fast = a.gred_off = a.rg_nit = 0;
+  a.dbg = a.cmp = 0;
+  a.stamps = nullptr;
   return a;
 }
 
@@ -576,6 +582,46 @@ inline bool rg_config(const dgprf_plan_t& pl, int l, bool fb, RgCfg& c) {
   return (int64_t)c.total * 4 <= 160 * 1024;
 }
 
+// Large minibatches with one chain: the step's forward is ONE launch of the predictive row / tile
+// kernel over all layers (k_forward_rows / k_forward_tiles, every layer's F kept on chip between
+// layers) writing complete F_l [B][g_l] into slice 0 of the F partial buffers, instead of L
+// feature-sliced launches whose 16 slice partials every consumer re-sums (16x the L2 reads).
+inline bool step_fused_fwd(const dgprf_plan_t& pl) {
+  return pl.rt_per_group > 1 && pl.n_chains == 1 && pl.a0_off < 0;
+}
+
+// Row-wave backward layout of layer l (step_bwdrw_impl.h; floats): false when the layer does not
+// fit it — it needs the fused forward's complete F_l (step_fused_fwd), >= 8 row tiles per group,
+// d <= 32, g <= 12, 4 or 8 chunks per slice and at most 8 gW accumulator tiles per wave.
+struct RwCfg {
+  int nch, wsa, osa, ost, wave0, wstride, hred, gred, total;
+};
+inline bool rw_config(const dgprf_plan_t& pl, int l, bool fb, RwCfg& c) {
+  const int d = pl.d[l], g = pl.n_gp[l], cpw = pl.cpw[l];
+  const int dxw = l > 0 ? pl.n_gp[l - 1] : 0;
+  const bool rbf = pl.kind[l] == DGPRF_RBF;
+  c.nch = 4 * cpw;
+  if (!step_fused_fwd(pl) || pl.rt_per_group < 8 || d > 32 || g > 12 || (c.nch != 4 && c.nch != 8) ||
+      c.nch * (rbf ? 2 : 1) > 8)
+    return false;
+  const int nf = 64 * cpw, xst = round4(d) + 1, dst = g + 1;
+  int off = 0;
+  c.wsa = off;
+  if (fb || dxw > 0) off += round4((rbf ? 2 : 1) * nf * g);
+  c.ost = nf + 4;
+  c.osa = off;
+  off += round4((d > dxw ? d : dxw) * c.ost);
+  c.wave0 = off;
+  c.wstride = round4(TR * xst) + 2 * round4(TR * dst);
+  off += 8 * c.wstride;
+  c.hred = off;
+  if (fb) off += 8 * round4(2 * d + 1);
+  c.gred = off;
+  off += 8 * (g == 1 ? c.nch * 2 * 64 : c.nch * 2 * 256);
+  c.total = off;
+  return (int64_t)c.total * 4 <= 160 * 1024;
+}
+
 // Kernel launch dispatch of the forward / backward over (NOT, G1, RBF, waves) for one A-tile k-step
 // count KS (each KS instantiated in its own translation unit, step_fwd_k<KS>.hip / step_bwd_k<KS>.hip).
 template <int KS>
@@ -584,6 +630,9 @@ void k_step_fwd_launch2(int g, bool rbf, int nw, dim3 grid, size_t lds, hipStrea
 template <int KS>
 void k_step_bwd_launch2(int g, bool rbf, bool fb, bool w8, dim3 grid, size_t lds, hipStream_t s,
                         const LayerK& a);
+template <int KS>
+void k_step_bwd_rw_launch2(int g, bool rbf, bool fb, int nch, dim3 grid, size_t lds,
+                           hipStream_t s, const LayerK& a);
 template <int KS>
 void k_step_bwd_rg_launch2(int g, bool rbf, bool fb, int nit, dim3 grid, size_t lds, hipStream_t s,
                            const LayerK& a);

@@ -28,9 +28,15 @@
 // fragment loads are unconditional with clamped addresses (no exec-masked branches or per-load
 // waits) and are issued before the dependent partial sums; minibatch rows of step t+1 are gathered
 // by step t's update kernel, so the forward never waits on the step counter or the permutation.
+#include <cstdlib>
+#define DGPRF_STAMPS_TU
+
 #include "step_common.h"
 
 namespace dgprf_sk {
+#ifdef DGPRF_STAMPS
+unsigned long long* rg_stamp_buffer();
+#endif
 
 struct GatherK {
   BatchDev bd;
@@ -589,6 +595,16 @@ void k_step_bwd_launch(int d, int g, bool rbf, bool fb, bool w8, dim3 grid, size
 using namespace dgprf_sk;
 
 #ifdef DGPRF_STAMPS
+// row-group backward stamps: a buffer of their own (17 x 4096 bases x 16 slots)
+static unsigned long long* g_rg_stamps = nullptr;
+unsigned long long* dgprf_sk::rg_stamp_buffer() {
+  if (!g_rg_stamps && hipMalloc(&g_rg_stamps, (size_t)17 * 4096 * 16 * 8) == hipSuccess)
+    (void)hipMemset(g_rg_stamps, 0, (size_t)17 * 4096 * 16 * 8);
+  return g_rg_stamps;
+}
+extern "C" int dgprf_debug_read_rg_stamps(unsigned long long* host, long long n) {
+  return g_rg_stamps && hipMemcpy(host, g_rg_stamps, (size_t)n * 8, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -3;
+}
 __device__ unsigned long long g_dgprf_stamps[17 * 4096 * DGPRF_STAMP_SLOTS];
 extern "C" int dgprf_debug_read_stamps(unsigned long long* host, long long n) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_dgprf_stamps), (size_t)n * 8, 0,
@@ -603,15 +619,29 @@ extern "C" int dgprf_debug_clear_stamps(void) {
 
 namespace dgprf {
 
-// A_1 = X Omega_1 of the step's gathered rows into the workspace (plan.a0_off): hipBLASLt, or
-// k_step_agemm when the library has no candidate for the shape (or its handle would have to be
-// created under stream capture).
+// Which A_1 GEMM runs: the hand-written MFMA kernel (agemm.hip) unless DGPRF_AGEMM=lib asks for
+// hipBLASLt (the comparison arm of scripts/diag/agemm_cmp.py); k_step_agemm for shapes outside both.
+static bool agemm_lib() {
+  static const int v = [] {
+    const char* e = getenv("DGPRF_AGEMM");
+    return e && e[0] == 'l' ? 1 : 0;
+  }();
+  return v != 0;
+}
+
+// A_1 = X Omega_1 of the step's gathered rows into the workspace (plan.a0_off).
 hipError_t launch_step_agemm(const dgprf_plan_t& pl, const StepDev& sd, hipStream_t s) {
   int lds_floats = 0;
   const LayerK a = make_layer_k(pl, sd, 0, lds_floats);
   if (!a.a0) return hipSuccess;
-  if (blas_agemm(a.xrows, pl.batch, pl.d_in, pl.d[0], a.om, pl.n_rf[0], sd.ws + pl.a0_off,
-                 pl.n_chains, a.xrow_cs, a.om_cs, pl.ws_chain, s))
+  hipError_t err = hipSuccess;
+  const int64_t rows = (pl.batch + 31) / 32 * 32;  // the [align32(B)][R] buffer, zero-padded
+  if (!agemm_lib() && own_agemm(a.xrows, pl.batch, rows, pl.d_in, pl.d[0], a.om, pl.n_rf[0],
+                                sd.ws + pl.a0_off, pl.n_chains, a.xrow_cs, a.om_cs, pl.ws_chain, s,
+                                &err))
+    return err;
+  if (agemm_lib() && blas_agemm(a.xrows, pl.batch, pl.d_in, pl.d[0], a.om, pl.n_rf[0],
+                                sd.ws + pl.a0_off, pl.n_chains, a.xrow_cs, a.om_cs, pl.ws_chain, s))
     return hipSuccess;
   AgemmK g;
   g.xrows = a.xrows;
@@ -648,7 +678,49 @@ hipError_t launch_step_fwd(const dgprf_plan_t& pl, const StepDev& sd, int layer,
   return hipGetLastError();
 }
 
+hipError_t launch_step_fwd_fused(const dgprf_plan_t& pl, const StepDev& sd, hipStream_t s) {
+  if (!step_fused_fwd(pl)) return hipErrorInvalidValue;
+  float* f_out[DGPRF_MAX_LAYERS];
+  for (int l = 0; l < DGPRF_MAX_LAYERS; ++l) f_out[l] = l < pl.n_layers ? sd.ws + pl.fp_off[l] : nullptr;
+  const bool direct = sd.bd.mode == DGPRF_BATCH_DIRECT;
+  const float* X = direct ? sd.bd.X : sd.ws + pl.xb_off;
+  // random_fixed=False layers: this step's Omega is the workspace copy (k_fresh_omega)
+  const float* om = pl.fresh_z && pl.omf_off >= 0 ? sd.ws + pl.omf_off : sd.omega;
+  return launch_forward_rows(pl, sd.theta, om, sd.der, X, nullptr, 0, pl.batch, f_out, nullptr,
+                             nullptr, nullptr, nullptr, nullptr, nullptr, s);
+}
+
 hipError_t launch_step_bwd(const dgprf_plan_t& pl, const StepDev& sd, int layer, hipStream_t s) {
+  RwCfg w;
+  static const bool no_rw = getenv("DGPRF_NO_RW") != nullptr;  // diagnostic: row-group kernel only
+  if (pl.rt_per_group > 1 && !no_rw && rw_config(pl, layer, sd.full_bayes != 0, w)) {
+    // row-wave backward (narrow slices after the fused forward): no barrier in the row-tile loop
+    int lds_floats = 0;
+    LayerK a = make_layer_k(pl, sd, layer, lds_floats, /*bwd=*/true, 4);
+    a.n_rt = pl.n_gw_rows;
+    a.rt_per_xcd = (pl.n_gw_rows + 7) / 8;
+    a.main_blocks = 8 * a.rt_per_xcd * a.ns;
+    a.rt_per_rg = pl.rt_per_group;
+    a.cmp = 1;
+    a.wsa_off = w.wsa;
+    a.osa_off = w.osa;
+    a.osa_st = w.ost;
+    a.aux_off = w.wave0;    // wave-private X / dF / Y tiles at aux_off + wave * red_off
+    a.red_off = w.wstride;
+    a.auxst = pl.n_gp[layer] + 1;
+    a.hred_off = w.hred;
+    a.gred_off = w.gred;
+    a.dsrc_off = a.last ? (int)pl.fp_off[layer] : (layer + 1 < pl.n_layers ? (int)pl.dxp_off[layer + 1] : 0);
+    dim3 grid(a.main_blocks, 1, pl.n_chains);
+    const int d = pl.d[layer], g = pl.n_gp[layer];
+    const bool rbf = pl.kind[layer] == DGPRF_RBF, fb = sd.full_bayes != 0;
+    const size_t lds = (size_t)w.total * sizeof(float);
+    if (d <= 4) k_step_bwd_rw_launch2<1>(g, rbf, fb, w.nch, grid, lds, s, a);
+    else if (d <= 8) k_step_bwd_rw_launch2<2>(g, rbf, fb, w.nch, grid, lds, s, a);
+    else if (d <= 16) k_step_bwd_rw_launch2<4>(g, rbf, fb, w.nch, grid, lds, s, a);
+    else k_step_bwd_rw_launch2<8>(g, rbf, fb, w.nch, grid, lds, s, a);
+    return hipGetLastError();
+  }
   if (pl.rt_per_group > 1) {  // row-group backward: at most 16 gW partial rows whatever B
     RgCfg c;
     if (!rg_config(pl, layer, sd.full_bayes != 0, c)) return hipErrorInvalidValue;
@@ -669,6 +741,11 @@ hipError_t launch_step_bwd(const dgprf_plan_t& pl, const StepDev& sd, int layer,
     a.osa_st = c.ost;
     a.hred_off = c.hred;
     a.gred_off = c.gred;
+    if (const char* dbg = getenv("DGPRF_DBG_RG")) a.dbg = atoi(dbg);
+    a.cmp = step_fused_fwd(pl) ? 1 : 0;
+#ifdef DGPRF_STAMPS
+    a.stamps = rg_stamp_buffer();
+#endif
     dim3 grid(a.main_blocks, 1, pl.n_chains);
     const int d = pl.d[layer], g = pl.n_gp[layer];
     const bool rbf = pl.kind[layer] == DGPRF_RBF, fb = sd.full_bayes != 0;
@@ -808,7 +885,11 @@ hipError_t launch_step_update(const dgprf_plan_t& pl, const StepDev& sd, const U
 hipError_t launch_agemm(const float* X, int64_t n, int ld, int d, const float* om, int R,
                         float* aout, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  if (n <= INT32_MAX && blas_agemm(X, n, ld, d, om, R, aout, 1, 0, 0, 0, s)) return hipSuccess;
+  hipError_t err = hipSuccess;
+  if (!agemm_lib() && n <= INT32_MAX && own_agemm(X, n, n, ld, d, om, R, aout, 1, 0, 0, 0, s, &err))
+    return err;
+  if (agemm_lib() && n <= INT32_MAX && blas_agemm(X, n, ld, d, om, R, aout, 1, 0, 0, 0, s))
+    return hipSuccess;
   if (n > INT32_MAX || (int64_t)n * ld >= ((int64_t)1 << 29) || (int64_t)d * R >= ((int64_t)1 << 29))
     return hipErrorInvalidValue;  // 32-bit buffer offsets
   AgemmK g;

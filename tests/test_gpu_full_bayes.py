@@ -321,18 +321,20 @@ def test_full_bayes_engine_grad_flags_and_scalar_lengthscale(dev, case):
     check_grad(eng, G, 0, O.grad_full(p, X, Y, N_, tr), tr)
 
 
-@pytest.mark.parametrize("case", [0, 1])
-def test_full_bayes_row_group_grad(dev, case):
-    """B = 600 (38 row tiles): the full-Bayes row-group backward keeps the hyper-parameter partials
-    per row group (<= 16 rows) like gW; every gradient against the oracle."""
+@pytest.mark.parametrize("case,B", [(0, 600), (1, 600), (0, 2048)])
+def test_full_bayes_row_group_grad(dev, case, B):
+    """B = 600 (38 row tiles: row-group kernel) and B = 2048 (8 row tiles per group: row-wave
+    kernel): the full-Bayes backward keeps the hyper-parameter partials per row group (<= 16 rows)
+    like gW; every gradient against the oracle."""
     spec_args, ard, flags = ENGINE_CASES[case]
     rng = np.random.default_rng(300 + case)
     eng = engine_for(spec_args, ard, flags)
     p = random_params(rng, spec_args, ard)
     load_chain(eng, p, 0)
-    B, N_ = 600, 5000
+    N_ = 5000
     pl = eng.plan_ws(B)[0]
-    assert pl.rt_per_group == 3 and pl.n_gw_rows == 13 and pl.rg_full_bayes == 1
+    n_rt = (B + 15) // 16
+    assert pl.rt_per_group == -(-n_rt // 16) and pl.n_gw_rows <= 16 and pl.rg_full_bayes == 1
     X = rng.standard_normal((B, spec_args[0]))
     Y = rng.standard_normal((B, spec_args[1])) if spec_args[6] == "gaussian" else \
         rng.integers(0, spec_args[1], (B, 1)).astype(float)

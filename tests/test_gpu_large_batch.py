@@ -41,6 +41,21 @@ def _oracle(m, kinds, n_rf, n_gp, d_in, cat, lik):
                     lik_log_var=np.log(0.3))
 
 
+def _rows_off_kinks(p, kinds, X, Y, n, tau=1e-5):
+    """The first n rows whose ARC-layer inner products all satisfy |A| >= tau in the float64
+    oracle: a row whose relu input sits within fp32 rounding of 0 can flip sides between the GPU's
+    forward and the oracle's and move the gradient by a whole feature's contribution (the same
+    selection as tests/test_gpu_configs.py)."""
+    _, cache = O.forward(p, X, keep=True)
+    ok = np.ones(X.shape[0], dtype=bool)
+    for l, k in enumerate(kinds):
+        if k == "ARC":
+            ok &= np.min(np.abs(cache[l][1]), axis=1) >= tau
+    idx = np.nonzero(ok)[0][:n]
+    assert len(idx) == n, "not enough rows away from the relu kink"
+    return X[idx], Y[idx]
+
+
 CASES = [
     # kinds, n_rf, n_gp, d_in, input_cat, likelihood, B      (what it exercises)
     (["RBF", "ARC", "RBF"], [64, 48, 40], [5, 3, 1], 7, False, "gaussian", 300),     # 4x4 waves, ragged group
@@ -48,7 +63,9 @@ CASES = [
     (["RBF", "RBF"], [4096, 1024], [30, 10], 40, False, "softmax", 520),             # A_1 GEMM layer, 2 out tiles
     (["RBF", "ARC"], [8192, 100], [16, 1], 16, False, "gaussian", 700),              # 2 chunks per wave, g = 1
     (["ARC", "RBF"], [64, 64], [16, 5], 40, True, "softmax", 400),                   # input_cat, wide d, 16 rows
-    (["RBF"] * 3, [1024] * 3, [8, 8, 1], 8, False, "gaussian", 8192),                # config 2 at B = 8192
+    (["RBF"] * 3, [1024] * 3, [8, 8, 1], 8, False, "gaussian", 8192),                # config 2 at B = 8192 (row-wave)
+    (["ARC"] * 3, [2048] * 3, [9, 9, 1], 9, False, "gaussian", 2048),                # config 3 shape, row-wave, 8 chunks
+    (["RBF", "ARC"], [1000, 200], [7, 3], 5, False, "softmax", 4000),                # row-wave, ragged R and groups
 ]
 
 
@@ -63,9 +80,10 @@ def test_row_group_gradient_matches_oracle(dev, case):
     assert pl.n_row_tiles == n_rt and pl.rt_per_group == (n_rt + 15) // 16 > 1
     assert pl.n_gw_rows == -(-n_rt // pl.rt_per_group) <= 16 and pl.n_rt_pad == 16
     rng = np.random.default_rng(case)
-    X = rng.standard_normal((B, d_in))
-    Y = rng.standard_normal((B, n_gp[-1])) if lik == "gaussian" else \
-        rng.integers(0, n_gp[-1], (B, 1)).astype(float)
+    X = rng.standard_normal((2 * B, d_in))
+    Y = rng.standard_normal((2 * B, n_gp[-1])) if lik == "gaussian" else \
+        rng.integers(0, n_gp[-1], (2 * B, 1)).astype(float)
+    X, Y = _rows_off_kinks(p, kinds, X, Y, B)
     N_ = 50_000
     G = unpack(eng, eng.grad(X, Y, N_))
     ref = O.grad_W(p, X, Y, N_)
