@@ -18,17 +18,36 @@
 
 namespace dgprf_sk {
 
-constexpr int RW_WAVES = 8;
+constexpr int RW_TS = 20;  // row stride of a wave's 16 x 16 transpose scratch (16-byte rows)
+
+// -DDGPRF_STAMPS diagnostic build only: s_memtime of lane 0 of a chosen wave into a.stamps
+#ifdef DGPRF_STAMPS
+#define RW_STAMP(cond, i)                                                               \
+  do {                                                                                 \
+    if ((cond) && (threadIdx.x & 63) == 0 && a.stamps) {                               \
+      __builtin_amdgcn_sched_barrier(0);                                               \
+      a.stamps[(size_t)stamp_base * 16 + (i)] = __builtin_amdgcn_s_memtime();          \
+      __builtin_amdgcn_sched_barrier(0);                                               \
+    }                                                                                  \
+  } while (0)
+#else
+#define RW_STAMP(cond, i) \
+  do {                    \
+  } while (0)
+#endif
 
 // NCH: 16-feature chunks of the slice (4 cpw); EX / ED: prefetched X / dF elements per lane
 // (16 dpad / 64, 16 g / 64 rounded up).
-template <int KS, int NOT, bool RBF, bool G1, bool FB, int NCH, int ED>
-__global__ __launch_bounds__(64 * RW_WAVES) void k_step_bwd_rw(const LayerK a) {
+template <int KS, int NOT, bool RBF, bool G1, bool FB, int NCH, int ED, int NWV>
+__global__ __launch_bounds__(64 * NWV) void k_step_bwd_rw(const LayerK a) {
   constexpr int EX = KS;  // 16 rows x 4 KS columns of X = KS elements per lane
   extern __shared__ __attribute__((aligned(16))) float smem[];
   int rg, sl;
   if (!tile_of_block(a, rg, sl)) return;
   const int chain = blockIdx.z;
+#ifdef DGPRF_STAMPS
+  const int stamp_base = (a.layer * 2 + 1) * 4096 + blockIdx.z * gridDim.x + blockIdx.x;
+#endif
   const float* __restrict__ om = a.om + (int64_t)chain * a.om_cs;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, lr = lane & 15, lq = lane >> 4;
   const int R = a.R, g = a.g, d = a.d, B = a.B, dxw = a.dxw;
@@ -46,7 +65,9 @@ __global__ __launch_bounds__(64 * RW_WAVES) void k_step_bwd_rw(const LayerK a) {
   float* xw = smem + a.aux_off + wave * a.red_off;  // wave-private: X [16][xst], dF, Y [16][dst]
   float* dw = xw + round4(TR * xst);
   float* yw = dw + round4(TR * dst);
+  float* tw = yw + round4(TR * dst);            // dA tile transpose scratch [16][RW_TS]
   const float cl = a.cptr[(int64_t)chain * a.der_cs];
+  RW_STAMP(wave == 0, 0);
 
   // ---- the slice's W rows (both halves) and Omega rows k < max(d, dxw), once (zero past R)
   {
@@ -150,10 +171,17 @@ __global__ __launch_bounds__(64 * RW_WAVES) void k_step_bwd_rw(const LayerK a) {
 
   float* dxp = a.dxout + (int64_t)chain * a.ws_cs + (int64_t)sl * B * dxw;
   __syncthreads();  // staged slice visible to every wave
+  RW_STAMP(wave == 0, 1);
   int rt = rt0 + wave;
-  if (rt < rt_end) issue(rt);
-  for (; rt < rt_end; rt += RW_WAVES) {
+  // 8 waves: the next row tile's loads are prefetched into registers while this one computes;
+  // 16 waves (four per SIMD, 128 VGPRs): no prefetch registers, the other waves hide the loads
+  constexpr bool PF = NWV == 8;
+  if (PF && rt < rt_end) issue(rt);
+  int it = 0;
+  for (; rt < rt_end; rt += NWV, ++it) {
     const int row0 = rt * TR;
+    RW_STAMP(wave == 0 && it < 4, 2 + 2 * it);
+    if (!PF) issue(rt);
     commit();
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes done
     __builtin_amdgcn_wave_barrier();
@@ -201,7 +229,7 @@ __global__ __launch_bounds__(64 * RW_WAVES) void k_step_bwd_rw(const LayerK a) {
       __builtin_amdgcn_wave_barrier();
     }
     // the next row tile's loads are in flight while this one computes
-    if (rt + RW_WAVES < rt_end) issue(rt + RW_WAVES);
+    if (PF && rt + NWV < rt_end) issue(rt + NWV);
     float xf[8];
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) xf[ks] = (ks < KS && 4 * ks < d) ? xw[lr * xst + 4 * ks + lq] : 0.f;
@@ -220,7 +248,6 @@ __global__ __launch_bounds__(64 * RW_WAVES) void k_step_bwd_rw(const LayerK a) {
         dfg[ot][r] = (o < g) ? dw[(4 * lq + r) * dst + o] : 0.f;
       }
     const int KG = (g + 3) >> 2;
-    const float dg1 = G1 ? dw[lr * dst] : 0.f;
     float dg4[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) dg4[r] = G1 ? dw[(4 * lq + r) * dst] : 0.f;
@@ -253,43 +280,48 @@ __global__ __launch_bounds__(64 * RW_WAVES) void k_step_bwd_rw(const LayerK a) {
           oxv[dt] = dt < ND ? *reinterpret_cast<const f4*>(osc + (dt * 16 + lr) * a.osa_st + 4 * lq)
                             : f4zero();
       }
+      // A tile in the rows-in-registers orientation: at_t[r] = A[row 4 lq + r][f0 + lr]
       const f4 at_t = a_tile<KS, true>(om, R, d, f0, omk, xf, xw, xst, lr, lq);
-      f4 at_n = f4zero(), dpc = f4zero(), dps = f4zero();
+      // dPhi in the same orientation: dpc[r] = dPhi_cos[row 4 lq + r][f0 + lr] = sum_o dF W
+      f4 dpc = f4zero(), dps = f4zero();
       if (dphi) {
-        at_n = a_tile<KS, false>(om, R, d, f0, omk, xf, xw, xst, lr, lq);
         if (G1) {
+          const bool ok = f0 + lr < R;
+          const float w0 = ok ? wsc[lr] : 0.f, w1 = (ok && RBF) ? wsc[whalf + lr] : 0.f;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int fl = c * 16 + 4 * lq + r;
-            const bool ok = f0 + 4 * lq + r < R;
-            dpc[r] = ok ? dg1 * wsa[fl] : 0.f;
-            dps[r] = (ok && RBF) ? dg1 * wsa[whalf + fl] : 0.f;
+            dpc[r] = dg4[r] * w0;
+            dps[r] = dg4[r] * w1;
           }
         } else {
 #pragma unroll
           for (int ks = 0; ks < KGM; ++ks)
             if (ks < KG) {
-              dpc = mfma16(wd0[ks], dff[ks], dpc);
-              if (RBF) dps = mfma16(wd1[ks], dff[ks], dps);
+              dpc = mfma16(dff[ks], wd0[ks], dpc);
+              if (RBF) dps = mfma16(dff[ks], wd1[ks], dps);
             }
         }
       }
       float q0[4], q1[4];
-      features<RBF>(at_t, cl, q0, q1);
+      features<RBF>(at_t, cl, q0, q1);  // q0 = c cos A | c relu A, q1 = c sin A
       float da[4];
       if (dphi) {
+        float dat[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           if (RBF) {
-            float sv, cv;
-            rf_sincos(at_n[r], &sv, &cv);
-            da[r] = -(cl * sv) * dpc[r] + (cl * cv) * dps[r];
-            if (FB) ampl += dpc[r] * (cl * cv) + dps[r] * (cl * sv);
+            dat[r] = -q1[r] * dpc[r] + q0[r] * dps[r];
+            if (FB) ampl += dpc[r] * q0[r] + dps[r] * q1[r];
           } else {
-            da[r] = at_n[r] > 0.f ? cl * dpc[r] : 0.f;
-            if (FB) ampl += dpc[r] * (cl * fmaxf(at_n[r], 0.f));
+            dat[r] = at_t[r] > 0.f ? cl * dpc[r] : 0.f;
+            if (FB) ampl += dpc[r] * q0[r];
           }
         }
+        // dA to the features-in-registers orientation of the dX / z contractions through the
+        // wave's LDS scratch: da[r] = dA[row lr][f0 + 4 lq + r]
+        *reinterpret_cast<f4*>(tw + lr * RW_TS + 4 * lq) = f4{dat[0], dat[1], dat[2], dat[3]};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) da[r] = tw[(4 * lq + r) * RW_TS + lr];
       }
       if (G1) {
         float gc = 0.f, gs = 0.f;
@@ -346,6 +378,7 @@ __global__ __launch_bounds__(64 * RW_WAVES) void k_step_bwd_rw(const LayerK a) {
         }
       }
     }
+    RW_STAMP(wave == 0 && it < 4, 3 + 2 * it);
     // dX rows of this tile: the slice's complete sum (dxa[dt][r] = dX[row lr][dt 16 + 4 lq + r])
     if (dxw > 0) {
       const int b = row0 + lr;
@@ -363,26 +396,37 @@ __global__ __launch_bounds__(64 * RW_WAVES) void k_step_bwd_rw(const LayerK a) {
     }
   }
 
-  // ---- the group's gW partial row: the 8 waves' accumulators summed in wave order
+  RW_STAMP(wave == 7, 10);
+  RW_STAMP(wave == 0, 11);
+  // ---- the group's gW partial row: the waves' accumulators summed in a fixed order — 8 LDS
+  // slots, slot w = wave w (+ wave w + 8 with 16 waves), then slots 0..7
   __syncthreads();
-  constexpr int GSZ = G1 ? NCH * 2 * 64 : NCH * NOT * 2 * 256;
+  RW_STAMP(wave == 0, 12);
+  constexpr int HN = RBF ? 2 : 1;  // cos | sin halves (RBF), one half (ARC)
+  constexpr int GSZ = G1 ? NCH * 2 * 64 : NCH * NOT * HN * 256;
+  constexpr int NSLOT = 8;
   float* gred = smem + a.gred_off;
-  {
-    float* gw = gred + wave * GSZ;
+  auto put = [&](bool add) {
+    float* gw = gred + (wave & (NSLOT - 1)) * GSZ;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       if (G1) {
-        gw[(c * 2) * 64 + lane] = g1c[c];
-        gw[(c * 2 + 1) * 64 + lane] = g1s[c];
+        float* p0 = gw + (c * 2) * 64 + lane;
+        float* p1 = gw + (c * 2 + 1) * 64 + lane;
+        *p0 = add ? *p0 + g1c[c] : g1c[c];
+        *p1 = add ? *p1 + g1s[c] : g1s[c];
       } else {
 #pragma unroll
         for (int ot = 0; ot < NOT; ++ot)
 #pragma unroll
-          for (int h = 0; h < 2; ++h)
-            *reinterpret_cast<f4*>(gw + ((c * NOT + ot) * 2 + h) * 256 + 4 * lane) = gacc[c][ot][h];
+          for (int h = 0; h < HN; ++h) {
+            f4* p = reinterpret_cast<f4*>(gw + ((c * NOT + ot) * HN + h) * 256 + 4 * lane);
+            *p = add ? *p + gacc[c][ot][h] : gacc[c][ot][h];
+          }
       }
     }
-  }
+  };
+  if (wave < NSLOT) put(false);
   if (FB) {
     float v = sum16(ampl);
     v += __shfl_xor(v, 16);
@@ -393,24 +437,27 @@ __global__ __launch_bounds__(64 * RW_WAVES) void k_step_bwd_rw(const LayerK a) {
     }
   }
   __syncthreads();
-  // every thread sums a strided share of the gW values in wave order and stores them
+  if (NWV > NSLOT) {
+    if (wave >= NSLOT) put(true);
+    __syncthreads();
+  }
+  // every thread sums a strided share of the gW values in slot order and stores them
   float* gwp = a.gwp + (int64_t)chain * a.ws_cs + (int64_t)rg * a.w_cs;
   if (G1) {
     for (int e = threadIdx.x; e < NCH * 2 * 16; e += blockDim.x) {
       const int c = e / 32, h = (e / 16) & 1, fl = e & 15;  // lanes 0..15 hold features fl
       float v = gred[(c * 2 + h) * 64 + fl];
-      for (int w = 1; w < RW_WAVES; ++w) v += gred[w * GSZ + (c * 2 + h) * 64 + fl];
+      for (int w = 1; w < NSLOT; ++w) v += gred[w * GSZ + (c * 2 + h) * 64 + fl];
       const int f = fb0 + c * 16 + fl;
       if (f < R && (h == 0 || RBF)) gwp[h * R + f] = v;
     }
   } else {
-    for (int e = threadIdx.x; e < NCH * NOT * 2 * 256; e += blockDim.x) {
-      // e = ((c NOT + ot) 2 + h) 256 + 4 lane + r: gacc[c][ot][h][r] of lane
+    for (int e = threadIdx.x; e < GSZ; e += blockDim.x) {
+      // e = ((c NOT + ot) HN + h) 256 + 4 lane + r: gacc[c][ot][h][r] of lane
       const int blk = e >> 8, within = e & 255, ln = within >> 2, r = within & 3;
-      const int h = blk & 1, ot = (blk >> 1) % NOT, c = (blk >> 1) / NOT;
-      if (h == 1 && !RBF) continue;
+      const int h = blk % HN, ot = (blk / HN) % NOT, c = (blk / HN) / NOT;
       float v = gred[e];
-      for (int w = 1; w < RW_WAVES; ++w) v += gred[w * GSZ + e];
+      for (int w = 1; w < NSLOT; ++w) v += gred[w * GSZ + e];
       // gacc[c][ot][h][r] of lane ln = gW[f0 + 4 (ln >> 4) + r][ot 16 + (ln & 15)] (half h)
       const int f = fb0 + c * 16 + 4 * (ln >> 4) + r, o = ot * 16 + (ln & 15);
       if (f < R && o < g) gwp[(int64_t)(h * R + f) * g + o] = v;
@@ -421,24 +468,25 @@ __global__ __launch_bounds__(64 * RW_WAVES) void k_step_bwd_rw(const LayerK a) {
     const float* h0 = smem + a.hred_off;
     for (int e = threadIdx.x; e < 2 * d + 1; e += blockDim.x) {
       float s = h0[e];
-      for (int w = 1; w < RW_WAVES; ++w) s += h0[w * hst + e];
+      for (int w = 1; w < NWV; ++w) s += h0[w * hst + e];
       hp[e] = s;
     }
     if (a.last && a.lik_fb && threadIdx.x == 0 && sl == 0) {
       float s = h0[2 * d + 1];
-      for (int w = 1; w < RW_WAVES; ++w) s += h0[w * hst + 2 * d + 1];
+      for (int w = 1; w < NWV; ++w) s += h0[w * hst + 2 * d + 1];
       a.hpl[(int64_t)chain * a.ws_cs + rg] = s;
     }
   }
+  RW_STAMP(wave == 0, 14);
 }
 
-template <int KS, int NOT, bool G1, int NCH, int ED>
+template <int KS, int NOT, bool G1, int NCH, int ED, int NWV>
 void k_step_bwd_rw_launch4(bool rbf, bool fb, dim3 grid, size_t lds, hipStream_t s, const LayerK& a) {
-#define DGPRF_BWDRW(R_, F_)                                                                       \
-  do {                                                                                           \
-    dgprf::set_lds_limit((const void*)k_step_bwd_rw<KS, NOT, R_, G1, F_, NCH, ED>, lds);        \
-    hipLaunchKernelGGL((k_step_bwd_rw<KS, NOT, R_, G1, F_, NCH, ED>), grid, dim3(64 * RW_WAVES),  \
-                       lds, s, a);                                                               \
+#define DGPRF_BWDRW(R_, F_)                                                                         \
+  do {                                                                                             \
+    dgprf::set_lds_limit((const void*)k_step_bwd_rw<KS, NOT, R_, G1, F_, NCH, ED, NWV>, lds);      \
+    hipLaunchKernelGGL((k_step_bwd_rw<KS, NOT, R_, G1, F_, NCH, ED, NWV>), grid, dim3(64 * NWV),    \
+                       lds, s, a);                                                                 \
   } while (0)
   if (rbf) {
     if (fb) DGPRF_BWDRW(true, true);
@@ -449,20 +497,19 @@ void k_step_bwd_rw_launch4(bool rbf, bool fb, dim3 grid, size_t lds, hipStream_t
   }
 #undef DGPRF_BWDRW
 }
-// g <= 12 (ED = ceil(16 g / 64) <= 3), 4 or 8 chunks per slice
-template <int KS>
-void k_step_bwd_rw_launch2(int g, bool rbf, bool fb, int nch, dim3 grid, size_t lds,
+template <int KS, int NWV>
+void k_step_bwd_rw_launch3(int g, bool rbf, bool fb, int nch, dim3 grid, size_t lds,
                            hipStream_t s, const LayerK& a) {
   const int ed = (16 * g + 63) / 64;
-#define DGPRF_RW_ED(G1_, NCH_)                                                         \
-  do {                                                                                \
-    if (ed <= 1) k_step_bwd_rw_launch4<KS, 1, G1_, NCH_, 1>(rbf, fb, grid, lds, s, a); \
-    else if (ed == 2) k_step_bwd_rw_launch4<KS, 1, G1_, NCH_, 2>(rbf, fb, grid, lds, s, a); \
-    else k_step_bwd_rw_launch4<KS, 1, G1_, NCH_, 3>(rbf, fb, grid, lds, s, a);         \
+#define DGPRF_RW_ED(G1_, NCH_)                                                                    \
+  do {                                                                                           \
+    if (ed <= 1) k_step_bwd_rw_launch4<KS, 1, G1_, NCH_, 1, NWV>(rbf, fb, grid, lds, s, a);       \
+    else if (ed == 2) k_step_bwd_rw_launch4<KS, 1, G1_, NCH_, 2, NWV>(rbf, fb, grid, lds, s, a);  \
+    else k_step_bwd_rw_launch4<KS, 1, G1_, NCH_, 3, NWV>(rbf, fb, grid, lds, s, a);               \
   } while (0)
   if (g == 1) {
-    if (nch == 4) k_step_bwd_rw_launch4<KS, 1, true, 4, 1>(rbf, fb, grid, lds, s, a);
-    else k_step_bwd_rw_launch4<KS, 1, true, 8, 1>(rbf, fb, grid, lds, s, a);
+    if (nch == 4) k_step_bwd_rw_launch4<KS, 1, true, 4, 1, NWV>(rbf, fb, grid, lds, s, a);
+    else k_step_bwd_rw_launch4<KS, 1, true, 8, 1, NWV>(rbf, fb, grid, lds, s, a);
   } else if (nch == 4) {
     DGPRF_RW_ED(false, 4);
   } else {
@@ -470,10 +517,17 @@ void k_step_bwd_rw_launch2(int g, bool rbf, bool fb, int nch, dim3 grid, size_t 
   }
 #undef DGPRF_RW_ED
 }
+// g <= 12 (ED = ceil(16 g / 64) <= 3), 4 or 8 chunks per slice, 8 or 16 waves
+template <int KS>
+void k_step_bwd_rw_launch2(int g, bool rbf, bool fb, int nch, int nwv, dim3 grid, size_t lds,
+                           hipStream_t s, const LayerK& a) {
+  if (nwv == 16) k_step_bwd_rw_launch3<KS, 16>(g, rbf, fb, nch, grid, lds, s, a);
+  else k_step_bwd_rw_launch3<KS, 8>(g, rbf, fb, nch, grid, lds, s, a);
+}
 
 }  // namespace dgprf_sk
 
 #ifdef DGPRF_KS
-template void dgprf_sk::k_step_bwd_rw_launch2<DGPRF_KS>(int, bool, bool, int, dim3, size_t,
+template void dgprf_sk::k_step_bwd_rw_launch2<DGPRF_KS>(int, bool, bool, int, int, dim3, size_t,
                                                         hipStream_t, const dgprf_sk::LayerK&);
 #endif

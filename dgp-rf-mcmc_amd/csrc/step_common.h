@@ -594,9 +594,9 @@ inline bool step_fused_fwd(const dgprf_plan_t& pl) {
 // fit it — it needs the fused forward's complete F_l (step_fused_fwd), >= 8 row tiles per group,
 // d <= 32, g <= 12, 4 or 8 chunks per slice and at most 8 gW accumulator tiles per wave.
 struct RwCfg {
-  int nch, wsa, osa, ost, wave0, wstride, hred, gred, total;
+  int nch, nwv, wsa, osa, ost, wave0, wstride, hred, gred, total;
 };
-inline bool rw_config(const dgprf_plan_t& pl, int l, bool fb, RwCfg& c) {
+inline bool rw_config(const dgprf_plan_t& pl, int l, bool fb, RwCfg& c, int max_nwv = 16) {
   const int d = pl.d[l], g = pl.n_gp[l], cpw = pl.cpw[l];
   const int dxw = l > 0 ? pl.n_gp[l - 1] : 0;
   const bool rbf = pl.kind[l] == DGPRF_RBF;
@@ -605,21 +605,25 @@ inline bool rw_config(const dgprf_plan_t& pl, int l, bool fb, RwCfg& c) {
       c.nch * (rbf ? 2 : 1) > 8)
     return false;
   const int nf = 64 * cpw, xst = round4(d) + 1, dst = g + 1;
-  int off = 0;
-  c.wsa = off;
-  if (fb || dxw > 0) off += round4((rbf ? 2 : 1) * nf * g);
-  c.ost = nf + 4;
-  c.osa = off;
-  off += round4((d > dxw ? d : dxw) * c.ost);
-  c.wave0 = off;
-  c.wstride = round4(TR * xst) + 2 * round4(TR * dst);
-  off += 8 * c.wstride;
-  c.hred = off;
-  if (fb) off += 8 * round4(2 * d + 1);
-  c.gred = off;
-  off += 8 * (g == 1 ? c.nch * 2 * 64 : c.nch * 2 * 256);
-  c.total = off;
-  return (int64_t)c.total * 4 <= 160 * 1024;
+  // 16 waves (four per SIMD) when every wave still gets >= 2 row tiles and the layout fits
+  for (c.nwv = pl.rt_per_group >= 32 && max_nwv >= 16 ? 16 : 8;; c.nwv = 8) {
+    int off = 0;
+    c.wsa = off;
+    if (fb || dxw > 0) off += round4((rbf ? 2 : 1) * nf * g);
+    c.ost = nf + 4;
+    c.osa = off;
+    off += round4((d > dxw ? d : dxw) * c.ost);
+    c.wave0 = off;  // per wave: X tile, dF tile, Y tile, dA transpose scratch [16][20]
+    c.wstride = round4(TR * xst) + 2 * round4(TR * dst) + TR * 20;
+    off += c.nwv * c.wstride;
+    c.hred = off;
+    if (fb) off += c.nwv * round4(2 * d + 1);
+    c.gred = off;  // 8 slots of gW accumulators
+    off += 8 * (g == 1 ? c.nch * 2 * 64 : c.nch * (rbf ? 2 : 1) * 256);
+    c.total = off;
+    if ((int64_t)c.total * 4 <= 160 * 1024) return true;
+    if (c.nwv == 8) return false;
+  }
 }
 
 // Kernel launch dispatch of the forward / backward over (NOT, G1, RBF, waves) for one A-tile k-step
@@ -631,7 +635,7 @@ template <int KS>
 void k_step_bwd_launch2(int g, bool rbf, bool fb, bool w8, dim3 grid, size_t lds, hipStream_t s,
                         const LayerK& a);
 template <int KS>
-void k_step_bwd_rw_launch2(int g, bool rbf, bool fb, int nch, dim3 grid, size_t lds,
+void k_step_bwd_rw_launch2(int g, bool rbf, bool fb, int nch, int nwv, dim3 grid, size_t lds,
                            hipStream_t s, const LayerK& a);
 template <int KS>
 void k_step_bwd_rg_launch2(int g, bool rbf, bool fb, int nit, dim3 grid, size_t lds, hipStream_t s,

@@ -693,7 +693,8 @@ hipError_t launch_step_fwd_fused(const dgprf_plan_t& pl, const StepDev& sd, hipS
 hipError_t launch_step_bwd(const dgprf_plan_t& pl, const StepDev& sd, int layer, hipStream_t s) {
   RwCfg w;
   static const bool no_rw = getenv("DGPRF_NO_RW") != nullptr;  // diagnostic: row-group kernel only
-  if (pl.rt_per_group > 1 && !no_rw && rw_config(pl, layer, sd.full_bayes != 0, w)) {
+  static const int rw_max = getenv("DGPRF_RW_NWV") ? atoi(getenv("DGPRF_RW_NWV")) : 16;  // diagnostic
+  if (pl.rt_per_group > 1 && !no_rw && rw_config(pl, layer, sd.full_bayes != 0, w, rw_max)) {
     // row-wave backward (narrow slices after the fused forward): no barrier in the row-tile loop
     int lds_floats = 0;
     LayerK a = make_layer_k(pl, sd, layer, lds_floats, /*bwd=*/true, 4);
@@ -711,14 +712,17 @@ hipError_t launch_step_bwd(const dgprf_plan_t& pl, const StepDev& sd, int layer,
     a.hred_off = w.hred;
     a.gred_off = w.gred;
     a.dsrc_off = a.last ? (int)pl.fp_off[layer] : (layer + 1 < pl.n_layers ? (int)pl.dxp_off[layer + 1] : 0);
+#ifdef DGPRF_STAMPS
+    a.stamps = rg_stamp_buffer();
+#endif
     dim3 grid(a.main_blocks, 1, pl.n_chains);
     const int d = pl.d[layer], g = pl.n_gp[layer];
     const bool rbf = pl.kind[layer] == DGPRF_RBF, fb = sd.full_bayes != 0;
     const size_t lds = (size_t)w.total * sizeof(float);
-    if (d <= 4) k_step_bwd_rw_launch2<1>(g, rbf, fb, w.nch, grid, lds, s, a);
-    else if (d <= 8) k_step_bwd_rw_launch2<2>(g, rbf, fb, w.nch, grid, lds, s, a);
-    else if (d <= 16) k_step_bwd_rw_launch2<4>(g, rbf, fb, w.nch, grid, lds, s, a);
-    else k_step_bwd_rw_launch2<8>(g, rbf, fb, w.nch, grid, lds, s, a);
+    if (d <= 4) k_step_bwd_rw_launch2<1>(g, rbf, fb, w.nch, w.nwv, grid, lds, s, a);
+    else if (d <= 8) k_step_bwd_rw_launch2<2>(g, rbf, fb, w.nch, w.nwv, grid, lds, s, a);
+    else if (d <= 16) k_step_bwd_rw_launch2<4>(g, rbf, fb, w.nch, w.nwv, grid, lds, s, a);
+    else k_step_bwd_rw_launch2<8>(g, rbf, fb, w.nch, w.nwv, grid, lds, s, a);
     return hipGetLastError();
   }
   if (pl.rt_per_group > 1) {  // row-group backward: at most 16 gW partial rows whatever B

@@ -294,6 +294,27 @@ class Engine:
         N.call("dgprf_omega_build", ctypes.byref(self.layout),
                ptr(self.z if z is None else z), ptr(self.hyp),
                ptr(self.omega if omega is None else omega), ptr(self.der), stream())
+        if z is None and omega is None:
+            self._omega_built_key = self._omega_key()
+
+    def _omega_key(self):
+        """What Omega / c / sigma^2 are built from, as seen by torch: the z and hyp buffers and
+        their version counters (every in-place write through them or their views — the kernel
+        parameter views, an optimizer's sub_ — bumps the counter).  Device-side full-Bayes steps
+        rewrite hyp and rebuild Omega together, so they leave the pair consistent."""
+        return (self.z.data_ptr(), self.z._version, self.hyp.data_ptr(), self.hyp._version)
+
+    def build_omega_if_stale(self):
+        """build_omega() unless nothing it reads changed since the last full build."""
+        if self.lik_log_var_source is not None:
+            src = self.lik_log_var_source()
+            if src is not None and src.data_ptr() != self.lik_log_var_view().data_ptr():
+                self.build_omega()  # a separate source tensor: copy it in every time
+                return True
+        if getattr(self, "_omega_built_key", None) == self._omega_key():
+            return False
+        self.build_omega()
+        return True
 
     # ---------------------------------------------------------------- hot path
     def _prep_batch(self, X, Y):

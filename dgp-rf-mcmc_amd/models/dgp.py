@@ -442,7 +442,8 @@ class DGP_RF(Module):
                                  temperature, k, sched, start_step, cycle_length,
                                  resample_in_cycle_head, perm_seed, full_bayes=bool(full_bayesian),
                                  fresh_z=fresh)
-        eng.build_omega()
+        # Omega, c, sigma^2 only when a hyper-parameter or z changed since the last build
+        eng.build_omega_if_stale()
         full, rest = divmod(int(n_steps), spg)
         plan = [(mk(spg), full)] if full else []
         if rest:

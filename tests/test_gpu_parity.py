@@ -335,6 +335,47 @@ def test_graph_replay_equals_eager_steps(dev):
     assert torch.equal(a._engine.mom, b._engine.mom)
 
 
+def test_sgmcmc_graphs_rebuild_omega_only_when_stale(dev):
+    """sgmcmc_graphs builds Omega / c / sigma^2 only when z or a hyper-parameter changed since the
+    last build (torch version counters of the packed buffers): a second call with nothing changed
+    builds nothing; an in-place hyper-parameter update (as the MCEM Adam applies it) or a new z
+    rebuilds, and the rebuilt Omega equals a from-scratch build."""
+    from likelihoods import Gaussian
+    from models.regression_model import RegressionDGP
+    from dgprf import engine as E
+    E.set_seed(12)
+    m = RegressionDGP(4, 1, n_hidden_layers=2, n_rf=40, n_gp=[3, 1], likelihood=Gaussian())
+    eng = m._engine
+    n = 640
+    X = torch.randn(n, 4, device=dev)
+    Y = torch.randn(n, 1, device=dev)
+    m.precond_update(None, n, precond_type="identity")
+    calls = []
+    orig = eng.build_omega
+    eng.build_omega = lambda *a, **k: (calls.append(1), orig(*a, **k))[1]
+    run = lambda: m.run_sgmcmc(X, Y, n, 8, batch_size=64, lr=0.01, momentum_decay=0.9,
+                               steps_per_graph=8)
+    run()
+    first = len(calls)
+    run()
+    assert len(calls) == first  # nothing changed: no rebuild
+    with torch.no_grad():
+        m.kernel_list[0].log_inv_length_scale.sub_(0.1)
+        m.likelihood.lik_log_var.add_(0.05)
+    run()
+    assert len(calls) == first + 1
+    om = torch.empty_like(eng.omega)
+    orig(z=eng.z, omega=om)
+    torch.cuda.synchronize()
+    assert torch.equal(om, eng.omega)
+    with torch.no_grad():
+        m.BNN.layers[0].z.mul_(1.5)
+    run()
+    assert len(calls) == first + 2
+    run()
+    assert len(calls) == first + 2
+
+
 def test_graph_fresh_z_random_fixed_false(dev):
     """random_fixed=False inside graph-replayed steps (layers/rf_layers.py:39-41): every step draws
     z ~ N(0,1) on the device from Philox (seed, sub = step, RNG_Z, tag = 1 + layer) and builds that
