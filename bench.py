@@ -32,6 +32,10 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "SGHMC steps/sec + predictive samples/sec, L=3 RF=1024 DGP, 1/2/4/8 GPU"
 FP32_MFMA_PEAK = 157.3e12   # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 dense peak (FLOP/s)
 HBM_PEAK = 8.0e12           # MI355X_MICROARCH.md: HBM3E spec (B/s)
+# MI355X_MICROARCH.md per-instruction table: v_sin_f32 / v_cos_f32 issue 8 cycles per 64-lane wave
+# instruction on a SIMD; 256 CUs x 4 SIMDs at the 2.4 GHz peak clock
+TRANS_PER_S = 1024 * 64 / 8 * 2.4e9
+PROFILES = os.path.join(ROOT, "profiles", "r03")   # this round's committed rocprofv3 evidence
 
 CFG = dict(L=3, n_rf=1024, n_gp=[8, 8, 1], D=8, N=1_000_000, B=200, N_test=100_000,
            variance=0.1, lr=0.01, beta=0.9, T=1.0)
@@ -129,33 +133,41 @@ def cpu_baseline(runs=5, warm=50, timed=1000, pred_samples=5):
             "note": "BLAS matmuls use the listed threads; numpy elementwise/trig is single-threaded"}
 
 
+def _short(name):
+    """Kernel name without 'void ', namespaces and the argument list (rocprofv3 CSV names)."""
+    import re
+    name = name.replace("void ", "").replace("(anonymous namespace)::", "")
+    name = re.sub(r"\([^()]*\)$", "", name)  # the parameter list
+    return re.sub(r"\w+::", "", name)
+
+
 def pmc_traffic(prefix):
     """HBM-side bytes per launch of the kernels named `prefix...` (dispatch-weighted mean), from the
-    committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes (profiles/r02/pmc_traffic.json, made by
+    committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes (profiles/r03/pmc_traffic.json, made by
     scripts/gpu_profile_round.sh; FETCH doubled per MI355X_MICROARCH.md §HBM).  None if absent."""
-    path = os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json")
+    path = os.path.join(PROFILES, "pmc_traffic.json")
     if not os.path.exists(path):
         return None
     with open(path) as fh:
         ks = json.load(fh)["kernels"]
-    sel = [v for k, v in ks.items() if k.startswith(prefix) and "dispatches" in v]
+    sel = [v for k, v in ks.items() if (_short(k) + "<").startswith(prefix + "<") and "dispatches" in v]
     n = sum(v["dispatches"] for v in sel)
     return round(sum(v["traffic"] * v["dispatches"] for v in sel) / n) if n else None
 
 
-def rocprof_avg_us(prefix):
-    """Dispatch-weighted average duration (us) of the kernels named `prefix...` in the committed
-    rocprofv3 --kernel-trace --stats summary of this bench (profiles/r02/kernel_stats_bench.csv);
+def rocprof_avg_us(prefix, fname="kernel_stats_bench.csv"):
+    """Dispatch-weighted average duration (us) of the kernels named `prefix<...>` in the committed
+    rocprofv3 --kernel-trace --stats summary of this bench (profiles/r03/kernel_stats_bench.csv);
     None if absent.  Traced durations include each dispatch's own launch overhead."""
     import csv
-    path = os.path.join(ROOT, "profiles", "r02", "kernel_stats_bench.csv")
+    path = os.path.join(PROFILES, fname)
     if not os.path.exists(path):
         return None
     n = tot = 0.0
     with open(path) as fh:
         for r in csv.DictReader(fh):
-            name = r["Name"].replace("void ", "").replace("(anonymous namespace)::", "")
-            if name.startswith(prefix + "<") or name.startswith(prefix + "("):
+            name = _short(r["Name"])
+            if name == prefix or name.startswith(prefix + "<"):
                 n += float(r["Calls"])
                 tot += float(r["TotalDurationNs"])
     return round(tot / n / 1e3, 3) if n else None
@@ -225,6 +237,63 @@ def bench_config(cfg, dev, rank, world, barrier_sync, max_over_ranks, steps):
     return out
 
 
+def launch_boundary_us(dev, n=400):
+    """Cost of one dependent kernel boundary inside a graph, measured live: a torch CUDA graph of
+    n back-to-back one-element kernels on one stream, replayed; device time per kernel."""
+    t = torch.zeros(1, device=dev)
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            t.add_(1.0)
+    torch.cuda.current_stream(dev).wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(n):
+            t.add_(1.0)
+    g.replay()
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    best = None
+    for _ in range(5):
+        e0.record()
+        g.replay()
+        e1.record()
+        torch.cuda.synchronize(dev)
+        v = e0.elapsed_time(e1) * 1e3 / n
+        best = v if best is None else min(best, v)
+    del g
+    return best
+
+
+def b_sweep(model, X, Y, N_, batches, d, R, P, g):
+    """SURVEY §8d B-sweep on the benchmark model: graph-replayed SGHMC steps at each minibatch size
+    (steps/s and the step's fraction of the fp32 MFMA peak from the algorithmic FLOPs)."""
+    out = {}
+    for B, k in batches:
+        run = dict(batch_size=B, lr=CFG["lr"], momentum_decay=CFG["beta"], temperature=CFG["T"],
+                   steps_per_graph=min(100, k), perm_seed=7)
+        plan = model.sgmcmc_graphs(X, Y, N_, k, **run)
+        for gph, _ in plan:
+            gph.launch()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        e0.record()
+        model.run_sgmcmc(X, Y, N_, k, **run)
+        e1.record()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        fw, bw = step_flops(B, d, R, P, g)
+        out[str(B)] = {"steps_per_s": round(k / dt, 1), "us_per_step": round(dt * 1e6 / k, 2),
+                       "us_per_step_events": round(e0.elapsed_time(e1) * 1e3 / k, 2),
+                       "step_mflop": round((sum(fw) + sum(bw)) / 1e6, 2),
+                       "step_mfma_frac": round((sum(fw) + sum(bw)) / (dt / k) / FP32_MFMA_PEAK, 4),
+                       "steps": k}
+    assert torch.isfinite(model._engine.theta).all(), "b-sweep chain diverged"
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -239,6 +308,7 @@ def main():
     ap.add_argument("--profile-reps", type=int, default=200)
     ap.add_argument("--other-configs", type=int, default=1)
     ap.add_argument("--other-steps", type=int, default=1000)
+    ap.add_argument("--b-sweep", type=int, default=1)
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -350,21 +420,35 @@ def main():
     upd_bytes = 4 * pl.w_total * (pl.n_row_tiles + 2 + 2 + 2)  # gW partials + theta/mom r/w
     dom = max(per_name, key=lambda k: per_name[k][0] * per_name[k][2])
     ms_dom, fl_dom, _ = per_name[dom]
+    # duration per launch: the committed rocprofv3 kernel trace of this bench when present (so
+    # frac recomputes from profiles/r03/), the live event measurement beside it
+    rp_us = rocprof_avg_us(dom)
+    use_us = rp_us if rp_us else ms_dom * 1e3
+    n_launch = 2 * len(d) + 1
+    bnd_us = launch_boundary_us(dev)
     roof = {"kernel": dom, "bound": "mfma",
-            "achieved": round(fl_dom / (ms_dom * 1e-3) / 1e12, 6),
+            "achieved": round(fl_dom / (use_us * 1e-6) / 1e12, 6),
             "peak": FP32_MFMA_PEAK / 1e12, "unit": "TFLOP/s",
-            "frac": round(fl_dom / (ms_dom * 1e-3) / FP32_MFMA_PEAK, 8),
+            "frac": round(fl_dom / (use_us * 1e-6) / FP32_MFMA_PEAK, 8),
             "traffic": pmc_traffic(dom),
-            "traffic_source": "profiles/r02/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE "
+            "traffic_source": "profiles/r03/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE "
                               "passes of this bench; bytes per launch incl. Infinity-Cache hits)",
-            "avg_launch_us": round(ms_dom * 1e3, 3),
+            "avg_launch_us": round(use_us, 3),
+            "duration_source": ("profiles/r03/kernel_stats_bench.csv: rocprofv3 --kernel-trace --stats "
+                                "of this bench, dispatch-weighted average of the kernel's instances"
+                                if rp_us else "live hipEvent measurement (no committed trace found)"),
             "flops_per_launch": int(fl_dom),
-            "method": "hipEvent pair around the kernel minus an empty pair (dgprf_profile_step)",
-            "rocprof_avg_launch_us": rocprof_avg_us(dom),
-            "rocprof_note": "profiles/r02/kernel_stats_bench.csv (rocprofv3 --kernel-trace of this bench); "
-                            "traced durations include each dispatch's launch overhead, the event "
-                            "difference is the in-kernel span; step_us_events / launches per step "
-                            "is the boundary-inclusive share",
+            "live_event_us": round(ms_dom * 1e3, 3),
+            "live_frac": round(fl_dom / (ms_dom * 1e-3) / FP32_MFMA_PEAK, 8),
+            "live_method": "hipEvent pair around the kernel on its launch stream minus an empty "
+                           "pair (dgprf_profile_step, 200 steps): the in-kernel span; the traced "
+                           "duration also holds the dispatch's launch and the tracer's completion "
+                           "signal (DESIGN.md §5)",
+            "launch_floor": {"launches_per_step": n_launch, "boundary_us": round(bnd_us, 3),
+                             "floor_us_per_step": round(n_launch * bnd_us, 3),
+                             "steps_per_s_ceiling": round(1e6 / (n_launch * bnd_us), 1),
+                             "method": "live: graph of 400 dependent one-element kernels replayed, "
+                                       "device time per kernel (best of 5)"},
             "step_us_events": round(step_ms_dev * 1e3, 3),
             "empty_pair_us": round(prof["empty"] * 1e3, 3),
             "step_kernel_us": {"fwd": [round(x * 1e3, 3) for x in att_fwd],
@@ -374,6 +458,7 @@ def main():
             "update_hbm_GBps": round(upd_bytes / (att_upd * 1e-3) / 1e9, 2),
             "regime": "latency-bound at B=200: 51.6 MFLOP/step; see DESIGN.md"}
     fp = pred_flops(CFG["N_test"], d, R, P, g)
+    n_trans = CFG["N_test"] * sum(2 * r for r in R)  # sin + cos per RBF feature per test row
     roof_pred = {"kernel": "k_forward_tiles", "bound": "mfma",
                  "achieved": round(fp / (pred_kernel_ms * 1e-3) / 1e12, 4),
                  "peak": FP32_MFMA_PEAK / 1e12, "unit": "TFLOP/s",
@@ -382,7 +467,13 @@ def main():
                  "algorithmic_bytes": int(4 * CFG["N_test"] * (CFG["D"] + 1 + 3 * 2)),
                  "avg_launch_us": round(pred_kernel_ms * 1e3, 2),
                  "rocprof_avg_launch_us": rocprof_avg_us("k_forward_tiles"),
-                 "flops_per_launch": int(fp)}
+                 "flops_per_launch": int(fp),
+                 "transcendental_ceiling": {
+                     "sin_cos_per_sample": int(n_trans), "rate_per_s": TRANS_PER_S,
+                     "floor_us": round(n_trans / TRANS_PER_S * 1e6, 2),
+                     "frac_of_sample_time": round(n_trans / TRANS_PER_S / (pred_kernel_ms * 1e-3), 4),
+                     "rate_source": "MI355X_MICROARCH.md: v_sin_f32 / v_cos_f32 8 issue cycles per "
+                                    "wave instruction, 1024 SIMDs, 2.4 GHz"}}
 
     # ---------------- many chains per GPU (aggregate chain-steps/s; extra, not `value`)
     multi = None
@@ -434,6 +525,11 @@ def main():
             other[f"config{cfg}"] = bench_config(cfg, dev, rank, world, barrier_sync,
                                                  max_over_ranks, args.other_steps)
 
+    sweep = None
+    if args.b_sweep:
+        sweep = b_sweep(model, X, Y, N_, [(200, 2000), (1024, 1000), (8192, 400), (65536, 100)],
+                        d, R, P, g)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(runs=args.cpu_runs)
@@ -461,6 +557,7 @@ def main():
                            "ms_per_sample": round(t_pred * 1e3 / args.pred_samples, 4)},
             "roofline": roof, "roofline_predictive": roof_pred, "cpu_baseline": cpu,
             "multi_chain": multi, "full_bayes": full_bayes, "other_configs": other or None,
+            "b_sweep": sweep,
             "device": torch.cuda.get_device_name(dev),
         }
         print(json.dumps(line), flush=True)

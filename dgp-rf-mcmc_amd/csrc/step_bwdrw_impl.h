@@ -128,7 +128,9 @@ __global__ __launch_bounds__(64 * NWV) void k_step_bwd_rw(const LayerK a) {
   const rsrc_t rws = make_rsrc(a.ws + (int64_t)chain * a.ws_cs, a.ws_cs);
   const rsrc_t rxd = make_rsrc(a.xrows + (int64_t)chain * a.xrow_cs, (int64_t)B * (d - a.gp));
   const rsrc_t ry = make_rsrc(a.yrows + (int64_t)chain * a.yrow_cs, (int64_t)B * a.y_cols);
-  const int nsl = a.last ? 1 : NSM;  // F_L complete (fused forward) / dX_{l+1} slice partials
+  // F_L complete (fused forward) / dX_{l+1} slice partials (a.dbg & 8: timing-only diagnostic
+  // reading one slice)
+  const int nsl = (a.last || (a.dbg & 8)) ? 1 : NSM;
   const int yc = a.likelihood == DGPRF_LIK_GAUSSIAN ? g : 1;
   float px[EX], pd[ED][NSM], py[ED];
   auto issue = [&](int rt) {
@@ -180,11 +182,12 @@ __global__ __launch_bounds__(64 * NWV) void k_step_bwd_rw(const LayerK a) {
   int it = 0;
   for (; rt < rt_end; rt += NWV, ++it) {
     const int row0 = rt * TR;
-    RW_STAMP(wave == 0 && it < 4, 2 + 2 * it);
+    RW_STAMP(wave == 0 && it < 3, 2 + 3 * it);
     if (!PF) issue(rt);
     commit();
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes done
     __builtin_amdgcn_wave_barrier();
+    RW_STAMP(wave == 0 && it < 3, 3 + 3 * it);
     if (a.last) {
       // likelihood gradient dF = -(1/B) dlogp/dF (likelihoods/gaussian.py:18-25, softmax.py:8-15)
       float lvrow = 0.f;
@@ -378,7 +381,7 @@ __global__ __launch_bounds__(64 * NWV) void k_step_bwd_rw(const LayerK a) {
         }
       }
     }
-    RW_STAMP(wave == 0 && it < 4, 3 + 2 * it);
+    RW_STAMP(wave == 0 && it < 3, 4 + 3 * it);
     // dX rows of this tile: the slice's complete sum (dxa[dt][r] = dX[row lr][dt 16 + 4 lq + r])
     if (dxw > 0) {
       const int b = row0 + lr;
@@ -396,7 +399,7 @@ __global__ __launch_bounds__(64 * NWV) void k_step_bwd_rw(const LayerK a) {
     }
   }
 
-  RW_STAMP(wave == 7, 10);
+  RW_STAMP(wave == NWV - 1, 13);
   RW_STAMP(wave == 0, 11);
   // ---- the group's gW partial row: the waves' accumulators summed in a fixed order — 8 LDS
   // slots, slot w = wave w (+ wave w + 8 with 16 waves), then slots 0..7

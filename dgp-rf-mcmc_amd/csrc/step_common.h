@@ -586,8 +586,10 @@ inline bool rg_config(const dgprf_plan_t& pl, int l, bool fb, RgCfg& c) {
 // kernel over all layers (k_forward_rows / k_forward_tiles, every layer's F kept on chip between
 // layers) writing complete F_l [B][g_l] into slice 0 of the F partial buffers, instead of L
 // feature-sliced launches whose 16 slice partials every consumer re-sums (16x the L2 reads).
+// From 8 row tiles per group (B > 1,792): below that the one-tile-per-workgroup forward leaves
+// most CUs idle (config 2 at B = 1,024: 59.7 us/step fused vs 48.8 per layer).
 inline bool step_fused_fwd(const dgprf_plan_t& pl) {
-  return pl.rt_per_group > 1 && pl.n_chains == 1 && pl.a0_off < 0;
+  return pl.rt_per_group >= 8 && pl.n_chains == 1 && pl.a0_off < 0;
 }
 
 // Row-wave backward layout of layer l (step_bwdrw_impl.h; floats): false when the layer does not

@@ -47,10 +47,11 @@ n = 17 * 4096 * 16
 buf = (ctypes.c_ulonglong * n)()
 assert f(ctypes.cast(buf, ctypes.c_void_p), n) == 0
 S = np.frombuffer(buf, dtype=np.uint64).reshape(17, 4096, 16).astype(np.int64)
-# row-wave kernel (k_step_bwd_rw): 0 start, 1 staged, 2+2i / 3+2i wave 0's row tile i start / end,
-# 10 wave 7's loop end, 11 wave 0's loop end, 12 after the barrier, 14 exit
+# row-wave kernel (k_step_bwd_rw): 0 start, 1 staged, 2+3i / 3+3i / 4+3i wave 0's row tile i start /
+# tile loaded / chunks done, 11 wave 0's loop end, 12 after the barrier, 13 the last wave's loop end,
+# 14 exit
 RW = len(sys.argv) > 2 and sys.argv[2] == "rw"
-slots = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 11, 12, 14] if RW else [0, 1, 2, 3, 4, 5, 6, 7, 14]
+slots = [0, 1, 2, 3, 4, 5, 6, 7, 11, 12, 14] if RW else [0, 1, 2, 3, 4, 5, 6, 7, 14]
 for l in range(3):
     s = S[2 * l + 1]
     live = s[:, 0] > 0
@@ -64,8 +65,8 @@ for l in range(3):
         d = s[:, b] - s[:, a]
         print(f"  slot {a:2d} -> {b:2d}: median {int(np.median(d)):7d}  max {int(d.max()):7d} cycles")
     if RW:
-        d = s[:, 10] - s[:, 11]
-        print(f"  wave 7 loop end - wave 0 loop end: median {int(np.median(d))}  max {int(d.max())}")
+        d = s[:, 13] - s[:, 11]
+        print(f"  last wave loop end - wave 0 loop end: median {int(np.median(d))}  max {int(d.max())}")
     tot = s[:, 14] - s[:, 0]
     print(f"  total median {int(np.median(tot))} max {int(tot.max())} cycles; "
           f"first start -> last end {int(s[:, 14].max() - t0)}")

@@ -4,6 +4,7 @@
 Every *counter_collection.csv under the DIRs is read; rows are (kernel, counter, value, dispatch).
 """
 import csv
+import re
 import glob
 import os
 import sys
@@ -25,7 +26,7 @@ def main():
                     if not (k and c and v):
                         continue
                     short = k.replace("void ", "").replace("(anonymous namespace)::", "")
-                    short = short.split("(")[0]
+                    short = re.sub(r"\w+::", "", short.split("(")[0])
                     acc[(short, c)] += float(v)
                     disp[(short, c)].add(i)
     with open(out, "w", newline="") as fh:
