@@ -38,7 +38,9 @@ constexpr int RW_TS = 20;  // row stride of a wave's 16 x 16 transpose scratch (
 
 // NCH: 16-feature chunks of the slice (4 cpw); EX / ED: prefetched X / dF elements per lane
 // (16 dpad / 64, 16 g / 64 rounded up).
-template <int KS, int NOT, bool RBF, bool G1, bool FB, int NCH, int ED, int NWV>
+// DX: the layer has a dX output (l > 0; dxw <= 16, one 16-wide dX tile).  Compile-time so the
+// chunk body carries no runtime branch: KG = ED dF k-steps, slices of whole chunks (R % nf == 0).
+template <int KS, int NOT, bool RBF, bool G1, bool FB, int NCH, int ED, int NWV, bool DX>
 __global__ __launch_bounds__(64 * NWV) void k_step_bwd_rw(const LayerK a) {
   constexpr int EX = KS;  // 16 rows x 4 KS columns of X = KS elements per lane
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -57,8 +59,8 @@ __global__ __launch_bounds__(64 * NWV) void k_step_bwd_rw(const LayerK a) {
   const int rt_end = min(rt0 + a.rt_per_rg, n_rt_all);
   const int row_end = min(rt_end * TR, B);
   constexpr int KGM = 4 * NOT;
-  const int ND = (dxw + 15) >> 4;
-  const bool dphi = FB || dxw > 0;
+  constexpr int KG = ED;  // dF k-steps: ceil(g / 4) (rw_config: ED = ceil(16 g / 64))
+  constexpr bool dphi = FB || DX;
   const int xst = a.xst, dst = a.auxst;
   float* wsa = smem + a.wsa_off;               // [RBF ? 2 : 1][nf][g]
   float* osa = smem + a.osa_off;               // [max(d, dxw)][osa_st]
@@ -250,15 +252,13 @@ __global__ __launch_bounds__(64 * NWV) void k_step_bwd_rw(const LayerK a) {
         const int o = ot * 16 + lr;
         dfg[ot][r] = (o < g) ? dw[(4 * lq + r) * dst + o] : 0.f;
       }
-    const int KG = (g + 3) >> 2;
     float dg4[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) dg4[r] = G1 ? dw[(4 * lq + r) * dst] : 0.f;
-    f4 dxa[2] = {f4zero(), f4zero()};
+    f4 dxa = f4zero();
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
-      const int f0 = fb0 + c * 16;
-      if (f0 >= R) break;  // wave-uniform
+      const int f0 = fb0 + c * 16;  // < R: slices hold whole chunks (rw_config)
       const float* wsc = wsa + c * 16 * g;
       const int whalf = nf * g;
       const float* osc = osa + c * 16;
@@ -268,29 +268,24 @@ __global__ __launch_bounds__(64 * NWV) void k_step_bwd_rw(const LayerK a) {
       for (int ks = 0; ks < 8; ++ks)
         omk[ks] = (ks < KS && 4 * ks + lq < d) ? osc[(4 * ks + lq) * a.osa_st + lr] : 0.f;
       float wd0[KGM], wd1[KGM];
-      f4 oxv[4];
+      f4 oxv = f4zero();
       if (dphi) {
-        const bool frow = f0 + lr < R;
 #pragma unroll
-        for (int ks = 0; ks < KGM; ++ks) {
+        for (int ks = 0; ks < KG; ++ks) {
           const int o = 4 * ks + lq, wo = lr * g + o;
-          const bool ok = o < g && frow;
+          const bool ok = o < g;
           wd0[ks] = G1 ? 0.f : (ok ? wsc[wo] : 0.f);
           wd1[ks] = (G1 || !RBF) ? 0.f : (ok ? wsc[whalf + wo] : 0.f);
         }
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt)
-          oxv[dt] = dt < ND ? *reinterpret_cast<const f4*>(osc + (dt * 16 + lr) * a.osa_st + 4 * lq)
-                            : f4zero();
       }
+      if (DX) oxv = *reinterpret_cast<const f4*>(osc + lr * a.osa_st + 4 * lq);
       // A tile in the rows-in-registers orientation: at_t[r] = A[row 4 lq + r][f0 + lr]
       const f4 at_t = a_tile<KS, true>(om, R, d, f0, omk, xf, xw, xst, lr, lq);
       // dPhi in the same orientation: dpc[r] = dPhi_cos[row 4 lq + r][f0 + lr] = sum_o dF W
       f4 dpc = f4zero(), dps = f4zero();
       if (dphi) {
         if (G1) {
-          const bool ok = f0 + lr < R;
-          const float w0 = ok ? wsc[lr] : 0.f, w1 = (ok && RBF) ? wsc[whalf + lr] : 0.f;
+          const float w0 = wsc[lr], w1 = RBF ? wsc[whalf + lr] : 0.f;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             dpc[r] = dg4[r] * w0;
@@ -298,11 +293,10 @@ __global__ __launch_bounds__(64 * NWV) void k_step_bwd_rw(const LayerK a) {
           }
         } else {
 #pragma unroll
-          for (int ks = 0; ks < KGM; ++ks)
-            if (ks < KG) {
-              dpc = mfma16(dff[ks], wd0[ks], dpc);
-              if (RBF) dps = mfma16(dff[ks], wd1[ks], dps);
-            }
+          for (int ks = 0; ks < KG; ++ks) {
+            dpc = mfma16(dff[ks], wd0[ks], dpc);
+            if (RBF) dps = mfma16(dff[ks], wd1[ks], dps);
+          }
         }
       }
       float q0[4], q1[4];
@@ -350,13 +344,9 @@ __global__ __launch_bounds__(64 * NWV) void k_step_bwd_rw(const LayerK a) {
             if (RBF) gacc[c][ot][1] = mfma16(q1[r], dfg[ot][r], gacc[c][ot][1]);
           }
       }
-      if (dxw > 0) {
+      if (DX) {
 #pragma unroll
-        for (int dt = 0; dt < 2; ++dt)
-          if (dt < ND) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) dxa[dt] = mfma16(oxv[dt][r], da[r], dxa[dt]);
-          }
+        for (int r = 0; r < 4; ++r) dxa = mfma16(oxv[r], da[r], dxa);
       }
       if (FB) {
         float rs = (da[0] + da[1]) + (da[2] + da[3]);
@@ -382,19 +372,15 @@ __global__ __launch_bounds__(64 * NWV) void k_step_bwd_rw(const LayerK a) {
       }
     }
     RW_STAMP(wave == 0 && it < 3, 4 + 3 * it);
-    // dX rows of this tile: the slice's complete sum (dxa[dt][r] = dX[row lr][dt 16 + 4 lq + r])
-    if (dxw > 0) {
+    // dX rows of this tile: the slice's complete sum (dxa[r] = dX[row lr][4 lq + r])
+    if (DX) {
       const int b = row0 + lr;
       if (b < row_end) {
 #pragma unroll
-        for (int dt = 0; dt < 2; ++dt)
-          if (dt < ND) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int k = dt * 16 + 4 * lq + r;
-              if (k < dxw) dxp[(int64_t)b * dxw + k] = dxa[dt][r];
-            }
-          }
+        for (int r = 0; r < 4; ++r) {
+          const int k = 4 * lq + r;
+          if (k < dxw) dxp[(int64_t)b * dxw + k] = dxa[r];
+        }
       }
     }
   }
@@ -483,54 +469,58 @@ __global__ __launch_bounds__(64 * NWV) void k_step_bwd_rw(const LayerK a) {
   RW_STAMP(wave == 0, 14);
 }
 
-template <int KS, int NOT, bool G1, int NCH, int ED, int NWV>
-void k_step_bwd_rw_launch4(bool rbf, bool fb, dim3 grid, size_t lds, hipStream_t s, const LayerK& a) {
-#define DGPRF_BWDRW(R_, F_)                                                                         \
+template <int KS, int NOT, bool G1, int NCH, int ED, int NWV, bool RBF>
+void k_step_bwd_rw_launch4(bool fb, bool dx, dim3 grid, size_t lds, hipStream_t s, const LayerK& a) {
+#define DGPRF_BWDRW(F_, D_)                                                                         \
   do {                                                                                             \
-    dgprf::set_lds_limit((const void*)k_step_bwd_rw<KS, NOT, R_, G1, F_, NCH, ED, NWV>, lds);      \
-    hipLaunchKernelGGL((k_step_bwd_rw<KS, NOT, R_, G1, F_, NCH, ED, NWV>), grid, dim3(64 * NWV),    \
-                       lds, s, a);                                                                 \
+    dgprf::set_lds_limit((const void*)k_step_bwd_rw<KS, NOT, RBF, G1, F_, NCH, ED, NWV, D_>, lds);  \
+    hipLaunchKernelGGL((k_step_bwd_rw<KS, NOT, RBF, G1, F_, NCH, ED, NWV, D_>), grid,               \
+                       dim3(64 * NWV), lds, s, a);                                                 \
   } while (0)
-  if (rbf) {
-    if (fb) DGPRF_BWDRW(true, true);
+  if (fb) {
+    if (dx) DGPRF_BWDRW(true, true);
     else DGPRF_BWDRW(true, false);
   } else {
-    if (fb) DGPRF_BWDRW(false, true);
+    if (dx) DGPRF_BWDRW(false, true);
     else DGPRF_BWDRW(false, false);
   }
 #undef DGPRF_BWDRW
 }
 template <int KS, int NWV>
-void k_step_bwd_rw_launch3(int g, bool rbf, bool fb, int nch, dim3 grid, size_t lds,
+void k_step_bwd_rw_launch3(int g, bool rbf, bool fb, bool dx, int nch, dim3 grid, size_t lds,
                            hipStream_t s, const LayerK& a) {
   const int ed = (16 * g + 63) / 64;
-#define DGPRF_RW_ED(G1_, NCH_)                                                                    \
-  do {                                                                                           \
-    if (ed <= 1) k_step_bwd_rw_launch4<KS, 1, G1_, NCH_, 1, NWV>(rbf, fb, grid, lds, s, a);       \
-    else if (ed == 2) k_step_bwd_rw_launch4<KS, 1, G1_, NCH_, 2, NWV>(rbf, fb, grid, lds, s, a);  \
-    else k_step_bwd_rw_launch4<KS, 1, G1_, NCH_, 3, NWV>(rbf, fb, grid, lds, s, a);               \
+  // RBF slices hold 4 chunks (8 accumulator tiles: cos | sin), ARC slices 4 or 8
+#define DGPRF_RW_ED(G1_, NCH_, R_)                                                                 \
+  do {                                                                                            \
+    if (G1_) k_step_bwd_rw_launch4<KS, 1, true, NCH_, 1, NWV, R_>(fb, dx, grid, lds, s, a);        \
+    else if (ed <= 1) k_step_bwd_rw_launch4<KS, 1, false, NCH_, 1, NWV, R_>(fb, dx, grid, lds, s, a); \
+    else if (ed == 2) k_step_bwd_rw_launch4<KS, 1, false, NCH_, 2, NWV, R_>(fb, dx, grid, lds, s, a); \
+    else k_step_bwd_rw_launch4<KS, 1, false, NCH_, 3, NWV, R_>(fb, dx, grid, lds, s, a);          \
   } while (0)
-  if (g == 1) {
-    if (nch == 4) k_step_bwd_rw_launch4<KS, 1, true, 4, 1, NWV>(rbf, fb, grid, lds, s, a);
-    else k_step_bwd_rw_launch4<KS, 1, true, 8, 1, NWV>(rbf, fb, grid, lds, s, a);
+  if (rbf) {
+    if (g == 1) DGPRF_RW_ED(true, 4, true);
+    else DGPRF_RW_ED(false, 4, true);
   } else if (nch == 4) {
-    DGPRF_RW_ED(false, 4);
+    if (g == 1) DGPRF_RW_ED(true, 4, false);
+    else DGPRF_RW_ED(false, 4, false);
   } else {
-    DGPRF_RW_ED(false, 8);
+    if (g == 1) DGPRF_RW_ED(true, 8, false);
+    else DGPRF_RW_ED(false, 8, false);
   }
 #undef DGPRF_RW_ED
 }
 // g <= 12 (ED = ceil(16 g / 64) <= 3), 4 or 8 chunks per slice, 8 or 16 waves
 template <int KS>
-void k_step_bwd_rw_launch2(int g, bool rbf, bool fb, int nch, int nwv, dim3 grid, size_t lds,
-                           hipStream_t s, const LayerK& a) {
-  if (nwv == 16) k_step_bwd_rw_launch3<KS, 16>(g, rbf, fb, nch, grid, lds, s, a);
-  else k_step_bwd_rw_launch3<KS, 8>(g, rbf, fb, nch, grid, lds, s, a);
+void k_step_bwd_rw_launch2(int g, bool rbf, bool fb, bool dx, int nch, int nwv, dim3 grid,
+                           size_t lds, hipStream_t s, const LayerK& a) {
+  if (nwv == 16) k_step_bwd_rw_launch3<KS, 16>(g, rbf, fb, dx, nch, grid, lds, s, a);
+  else k_step_bwd_rw_launch3<KS, 8>(g, rbf, fb, dx, nch, grid, lds, s, a);
 }
 
 }  // namespace dgprf_sk
 
 #ifdef DGPRF_KS
-template void dgprf_sk::k_step_bwd_rw_launch2<DGPRF_KS>(int, bool, bool, int, int, dim3, size_t,
-                                                        hipStream_t, const dgprf_sk::LayerK&);
+template void dgprf_sk::k_step_bwd_rw_launch2<DGPRF_KS>(int, bool, bool, bool, int, int, dim3,
+                                                        size_t, hipStream_t, const dgprf_sk::LayerK&);
 #endif

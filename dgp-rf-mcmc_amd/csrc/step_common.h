@@ -603,10 +603,10 @@ inline bool rw_config(const dgprf_plan_t& pl, int l, bool fb, RwCfg& c, int max_
   const int dxw = l > 0 ? pl.n_gp[l - 1] : 0;
   const bool rbf = pl.kind[l] == DGPRF_RBF;
   c.nch = 4 * cpw;
-  if (!step_fused_fwd(pl) || pl.rt_per_group < 8 || d > 32 || g > 12 || (c.nch != 4 && c.nch != 8) ||
-      c.nch * (rbf ? 2 : 1) > 8)
-    return false;
   const int nf = 64 * cpw, xst = round4(d) + 1, dst = g + 1;
+  if (!step_fused_fwd(pl) || pl.rt_per_group < 8 || d > 32 || g > 12 || dxw > 16 ||
+      (c.nch != 4 && c.nch != 8) || c.nch * (rbf ? 2 : 1) > 8 || pl.n_rf[l] % nf != 0)
+    return false;
   // 16 waves (four per SIMD) when every wave still gets >= 2 row tiles and the layout fits
   for (c.nwv = pl.rt_per_group >= 32 && max_nwv >= 16 ? 16 : 8;; c.nwv = 8) {
     int off = 0;
@@ -637,7 +637,7 @@ template <int KS>
 void k_step_bwd_launch2(int g, bool rbf, bool fb, bool w8, dim3 grid, size_t lds, hipStream_t s,
                         const LayerK& a);
 template <int KS>
-void k_step_bwd_rw_launch2(int g, bool rbf, bool fb, int nch, int nwv, dim3 grid, size_t lds,
+void k_step_bwd_rw_launch2(int g, bool rbf, bool fb, bool dx, int nch, int nwv, dim3 grid, size_t lds,
                            hipStream_t s, const LayerK& a);
 template <int KS>
 void k_step_bwd_rg_launch2(int g, bool rbf, bool fb, int nit, dim3 grid, size_t lds, hipStream_t s,

@@ -720,10 +720,10 @@ hipError_t launch_step_bwd(const dgprf_plan_t& pl, const StepDev& sd, int layer,
     const int d = pl.d[layer], g = pl.n_gp[layer];
     const bool rbf = pl.kind[layer] == DGPRF_RBF, fb = sd.full_bayes != 0;
     const size_t lds = (size_t)w.total * sizeof(float);
-    if (d <= 4) k_step_bwd_rw_launch2<1>(g, rbf, fb, w.nch, w.nwv, grid, lds, s, a);
-    else if (d <= 8) k_step_bwd_rw_launch2<2>(g, rbf, fb, w.nch, w.nwv, grid, lds, s, a);
-    else if (d <= 16) k_step_bwd_rw_launch2<4>(g, rbf, fb, w.nch, w.nwv, grid, lds, s, a);
-    else k_step_bwd_rw_launch2<8>(g, rbf, fb, w.nch, w.nwv, grid, lds, s, a);
+    if (d <= 4) k_step_bwd_rw_launch2<1>(g, rbf, fb, layer > 0, w.nch, w.nwv, grid, lds, s, a);
+    else if (d <= 8) k_step_bwd_rw_launch2<2>(g, rbf, fb, layer > 0, w.nch, w.nwv, grid, lds, s, a);
+    else if (d <= 16) k_step_bwd_rw_launch2<4>(g, rbf, fb, layer > 0, w.nch, w.nwv, grid, lds, s, a);
+    else k_step_bwd_rw_launch2<8>(g, rbf, fb, layer > 0, w.nch, w.nwv, grid, lds, s, a);
     return hipGetLastError();
   }
   if (pl.rt_per_group > 1) {  // row-group backward: at most 16 gW partial rows whatever B

@@ -228,8 +228,12 @@ class Engine:
         key = (int(B), int(fresh_z))
         if key not in self._ws:
             pl = self.spec.plan(key[0], self.C, self.per_chain_hyp)
-            if fresh_z:
+            # fresh z layers; a forward path pinned by set_forward_path also pins the step's
+            # all-layer forward (large minibatches)
+            if fresh_z or self.layout.fwd_path != N.FWD_AUTO:
                 pl.fresh_z = key[1]
+                pl.fwd_path = self.layout.fwd_path
+                pl.agemm_chunk_rows = self.layout.agemm_chunk_rows
                 N.call("dgprf_plan_init", ctypes.byref(pl))
             ws = torch.zeros(max(pl.ws_total, 4), dtype=_F32, device=self.dev)
             self._ws[key] = (pl, ws)

@@ -18,6 +18,13 @@ for line in sys.stdin:
 names = subprocess.run(["c++filt"], input="\n".join(r["name"] for r in rows), capture_output=True,
                        text=True).stdout.split("\n")
 for r, n in zip(rows, names):
-    n = re.sub(r"\(.*\)$", "", n.replace("void ", "")).replace("dgprf_sk::", "")
+    n = n.replace("void ", "").replace("(anonymous namespace)::", "").replace("dgprf_sk::", "")
+    if n.endswith(")"):  # drop the parameter list (match the closing parenthesis)
+        depth = 0
+        for i in range(len(n) - 1, -1, -1):
+            depth += {")": 1, "(": -1}.get(n[i], 0)
+            if depth == 0:
+                n = n[:i]
+                break
     print(f"v{r.get('VGPRs', '?'):>4} a{r.get('AGPRs', '?'):>3} spill {r.get('VGPRs Spill', '?'):>4} "
           f"lds {r.get('LDS Size [bytes/block]', '?'):>6} occ {r.get('Occupancy [waves/SIMD]', '?'):>2}  {n}")
