@@ -61,9 +61,10 @@ __global__ __launch_bounds__(64 * NWV) void k_step_bwd_rw(const LayerK a) {
   constexpr int KGM = 4 * NOT;
   constexpr int KG = ED;  // dF k-steps: ceil(g / 4) (rw_config: ED = ceil(16 g / 64))
   constexpr bool dphi = FB || DX;
-  const int xst = a.xst, dst = a.auxst;
-  float* wsa = smem + a.wsa_off;               // [RBF ? 2 : 1][nf][g]
-  float* osa = smem + a.osa_off;               // [max(d, dxw)][osa_st]
+  constexpr int GPW = G1 ? 1 : 4 * KG;  // W staging row width (outputs, zero past g)
+  const int xst = a.xst, dst = a.auxst;  // 4 KS + 1, 17 (rw_config)
+  float* wsa = smem + a.wsa_off;               // [RBF ? 2 : 1][nf][GPW]
+  float* osa = smem + a.osa_off;               // [max(4 KS, d)][osa_st], zero rows past d
   float* xw = smem + a.aux_off + wave * a.red_off;  // wave-private: X [16][xst], dF, Y [16][dst]
   float* dw = xw + round4(TR * xst);
   float* yw = dw + round4(TR * dst);
@@ -71,32 +72,24 @@ __global__ __launch_bounds__(64 * NWV) void k_step_bwd_rw(const LayerK a) {
   const float cl = a.cptr[(int64_t)chain * a.der_cs];
   RW_STAMP(wave == 0, 0);
 
-  // ---- the slice's W rows (both halves) and Omega rows k < max(d, dxw), once (zero past R)
+  // ---- the slice's W rows (both halves, outputs zero-padded to GPW) and Omega rows (zero past
+  // d), once; the slice holds whole chunks (R % nf == 0)
   {
     const float* W = a.W + (int64_t)chain * a.w_cs;
-    const int nh = RBF ? 2 : 1, nwf = nf * g;
-    if (dphi) {
-      if (((int64_t)R * g) % 4 == 0) {
-        const int n4 = nwf / 4;
-        for (int e = threadIdx.x; e < nh * n4; e += blockDim.x) {
-          const int h = e >= n4, e2 = 4 * (e - h * n4);
-          f4 v = f4zero();
-          if (fb0 + (e2 + 3) / g < R) v = *reinterpret_cast<const f4*>(W + ((int64_t)h * R + fb0) * g + e2);
-          *reinterpret_cast<f4*>(wsa + h * nwf + e2) = v;
-        }
-      } else {
-        for (int e = threadIdx.x; e < nh * nwf; e += blockDim.x) {
-          const int h = e >= nwf, e2 = e - h * nwf;
-          wsa[e] = fb0 + e2 / g < R ? W[((int64_t)h * R + fb0) * g + e2] : 0.f;
-        }
+    constexpr int NH = RBF ? 2 : 1;
+    if (dphi)
+      for (int e = threadIdx.x; e < NH * nf * GPW; e += blockDim.x) {
+        const int h = e / (nf * GPW), r2 = e - h * nf * GPW, f = r2 / GPW, o = r2 - f * GPW;
+        wsa[e] = o < g ? W[((int64_t)h * R + fb0 + f) * g + o] : 0.f;
       }
-    }
-    const int orows = d > dxw ? d : dxw;
+    const int orows = a.rw_orows > dxw ? a.rw_orows : dxw;
     for (int e = threadIdx.x; e < orows * nf; e += blockDim.x) {
       const int k = e / nf, c = e - k * nf;
-      osa[k * a.osa_st + c] = fb0 + c < R ? om[(int64_t)k * R + fb0 + c] : 0.f;
+      osa[k * a.osa_st + c] = k < d ? om[(int64_t)k * R + fb0 + c] : 0.f;
     }
   }
+  // the wave's tiles: zero once, so the X columns >= d and dF / Y columns >= g read as zeros
+  for (int e = lane; e < round4(TR * xst) + 2 * round4(TR * dst); e += 64) xw[e] = 0.f;
   constexpr int NZ = (4 * KS + 15) / 16;
   const rsrc_t rz = make_rsrc(a.z, FB ? (int64_t)d * R : 0);
   f4 zpf[NCH][FB ? NZ : 1];
@@ -237,21 +230,15 @@ __global__ __launch_bounds__(64 * NWV) void k_step_bwd_rw(const LayerK a) {
     if (PF && rt + NWV < rt_end) issue(rt + NWV);
     float xf[8];
 #pragma unroll
-    for (int ks = 0; ks < 8; ++ks) xf[ks] = (ks < KS && 4 * ks < d) ? xw[lr * xst + 4 * ks + lq] : 0.f;
+    for (int ks = 0; ks < 8; ++ks) xf[ks] = ks < KS ? xw[lr * xst + 4 * ks + lq] : 0.f;
     float dff[KGM];
 #pragma unroll
-    for (int ks = 0; ks < KGM; ++ks) {
-      const int o = 4 * ks + lq;
-      dff[ks] = (o < g) ? dw[lr * dst + o] : 0.f;
-    }
+    for (int ks = 0; ks < KG; ++ks) dff[ks] = dw[lr * dst + 4 * ks + lq];  // zero past g
     float dfg[NOT][4];
 #pragma unroll
     for (int ot = 0; ot < NOT; ++ot)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int o = ot * 16 + lr;
-        dfg[ot][r] = (o < g) ? dw[(4 * lq + r) * dst + o] : 0.f;
-      }
+      for (int r = 0; r < 4; ++r) dfg[ot][r] = dw[(4 * lq + r) * dst + ot * 16 + lr];
     float dg4[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) dg4[r] = G1 ? dw[(4 * lq + r) * dst] : 0.f;
@@ -259,23 +246,22 @@ __global__ __launch_bounds__(64 * NWV) void k_step_bwd_rw(const LayerK a) {
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int f0 = fb0 + c * 16;  // < R: slices hold whole chunks (rw_config)
-      const float* wsc = wsa + c * 16 * g;
-      const int whalf = nf * g;
+      const float* wsc = wsa + c * 16 * GPW;
+      const int whalf = nf * GPW;
       const float* osc = osa + c * 16;
       // Omega fragments of the A tile from the staged rows: omk[ks] = Omega[4 ks + lq][f0 + lr]
       float omk[8];
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks)
-        omk[ks] = (ks < KS && 4 * ks + lq < d) ? osc[(4 * ks + lq) * a.osa_st + lr] : 0.f;
+        omk[ks] = ks < KS ? osc[(4 * ks + lq) * a.osa_st + lr] : 0.f;  // zero rows past d
       float wd0[KGM], wd1[KGM];
       f4 oxv = f4zero();
       if (dphi) {
 #pragma unroll
         for (int ks = 0; ks < KG; ++ks) {
-          const int o = 4 * ks + lq, wo = lr * g + o;
-          const bool ok = o < g;
-          wd0[ks] = G1 ? 0.f : (ok ? wsc[wo] : 0.f);
-          wd1[ks] = (G1 || !RBF) ? 0.f : (ok ? wsc[whalf + wo] : 0.f);
+          const int wo = lr * GPW + 4 * ks + lq;
+          wd0[ks] = G1 ? 0.f : wsc[wo];
+          wd1[ks] = (G1 || !RBF) ? 0.f : wsc[whalf + wo];
         }
       }
       if (DX) oxv = *reinterpret_cast<const f4*>(osc + lr * a.osa_st + 4 * lq);

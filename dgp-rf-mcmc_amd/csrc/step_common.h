@@ -81,6 +81,7 @@ struct LayerK {
   // row-group backward (k_step_bwd_rg, minibatches of > 16 row tiles): rt_per_rg row tiles per
   // workgroup, ncw chunk-waves x nrw row-waves, register-prefetched prologue when rg_fast
   int32_t rt_per_rg, ncw, nrw, rg_fast, gred_off, rg_nit;
+  int32_t rw_orows, rw_pad;  // row-wave backward: staged Omega rows (zero past d)
   int32_t dbg;           // diagnostic switches (DGPRF_DBG env, never set in the product)
   int32_t cmp;           // row-group backward after the fused forward (step_fused_fwd): every
                          // F_l is complete in slice 0 of its partial buffer (one load, not 16)
@@ -537,6 +538,7 @@ inline LayerK make_layer_k(const dgprf_plan_t& pl, const StepDev& sd, int l, int
   a.rt_per_rg = 1;
   a.ncw = a.nrw = a.rg_fast = a.gred_off = a.rg_nit = 0;
   a.dbg = a.cmp = 0;
+  a.rw_orows = a.rw_pad = 0;
   a.stamps = nullptr;
   return a;
 }
@@ -597,24 +599,36 @@ inline bool step_fused_fwd(const dgprf_plan_t& pl) {
 // d <= 32, g <= 12, 4 or 8 chunks per slice and at most 8 gW accumulator tiles per wave.
 struct RwCfg {
   int nch, nwv, wsa, osa, ost, wave0, wstride, hred, gred, total;
+  int xst, dst, gpw, orows;  // X / dF tile row strides, W staging row width, staged Omega rows
 };
+// A-tile k-steps of the step kernels for input width d (the KS instance a layer runs)
+__host__ __device__ inline int step_ks(int d) { return d <= 4 ? 1 : (d <= 8 ? 2 : (d <= 16 ? 4 : 8)); }
 inline bool rw_config(const dgprf_plan_t& pl, int l, bool fb, RwCfg& c, int max_nwv = 16) {
   const int d = pl.d[l], g = pl.n_gp[l], cpw = pl.cpw[l];
   const int dxw = l > 0 ? pl.n_gp[l - 1] : 0;
   const bool rbf = pl.kind[l] == DGPRF_RBF;
   c.nch = 4 * cpw;
-  const int nf = 64 * cpw, xst = round4(d) + 1, dst = g + 1;
+  const int nf = 64 * cpw;
+  // zero-padded wave tiles and staging, so no fragment read in the chunk body is masked: X rows
+  // of 4 KS columns, dF / Y rows of 16 columns, W rows of 4 ceil(g / 4) outputs (1 for g = 1),
+  // Omega rows up to 4 KS
+  c.xst = 4 * step_ks(d) + 1;
+  c.dst = 17;
+  c.gpw = g == 1 ? 1 : 4 * ((g + 3) / 4);
+  c.orows = 4 * step_ks(d) > d ? 4 * step_ks(d) : d;
+  const int xst = c.xst, dst = c.dst;
   if (!step_fused_fwd(pl) || pl.rt_per_group < 8 || d > 32 || g > 12 || dxw > 16 ||
       (c.nch != 4 && c.nch != 8) || c.nch * (rbf ? 2 : 1) > 8 || pl.n_rf[l] % nf != 0)
     return false;
   // 16 waves (four per SIMD) when every wave still gets >= 2 row tiles and the layout fits
-  for (c.nwv = pl.rt_per_group >= 32 && max_nwv >= 16 ? 16 : 8;; c.nwv = 8) {
+  // (W-only steps: the full-Bayes body does not fit 128 VGPRs)
+  for (c.nwv = pl.rt_per_group >= 32 && max_nwv >= 16 && !fb ? 16 : 8;; c.nwv = 8) {
     int off = 0;
     c.wsa = off;
-    if (fb || dxw > 0) off += round4((rbf ? 2 : 1) * nf * g);
+    if (fb || dxw > 0) off += round4((rbf ? 2 : 1) * nf * c.gpw);
     c.ost = nf + 4;
     c.osa = off;
-    off += round4((d > dxw ? d : dxw) * c.ost);
+    off += round4((c.orows > dxw ? c.orows : dxw) * c.ost);
     c.wave0 = off;  // per wave: X tile, dF tile, Y tile, dA transpose scratch [16][20]
     c.wstride = round4(TR * xst) + 2 * round4(TR * dst) + TR * 20;
     off += c.nwv * c.wstride;

@@ -709,7 +709,9 @@ hipError_t launch_step_bwd(const dgprf_plan_t& pl, const StepDev& sd, int layer,
     a.osa_st = w.ost;
     a.aux_off = w.wave0;    // wave-private X / dF / Y tiles at aux_off + wave * red_off
     a.red_off = w.wstride;
-    a.auxst = pl.n_gp[layer] + 1;
+    a.auxst = w.dst;  // zero-padded wave tiles (rw_config)
+    a.xst = w.xst;
+    a.rw_orows = w.orows;
     a.hred_off = w.hred;
     a.gred_off = w.gred;
     a.dsrc_off = a.last ? (int)pl.fp_off[layer] : (layer + 1 < pl.n_layers ? (int)pl.dxp_off[layer + 1] : 0);
