@@ -209,6 +209,17 @@ def bench_config(cfg, dev, rank, world, barrier_sync, max_over_ranks, steps):
     L = len(c["kinds"])
     d, R, P, g = list(pl.d[:L]), list(pl.n_rf[:L]), list(pl.P[:L]), list(pl.n_gp[:L])
     fwd_f, bwd_f = step_flops(c["batch"], d, R, P, g)
+    a1 = None
+    if pl.a0_off >= 0:  # wide first layer: the A_1 = X Omega_1 GEMM timed apart (hipEvents)
+        prof = m._engine.profile_step(X, Y, c["batch"], n, c["lr"], c["beta"], c["T"], reps=100)
+        a1_us = max(prof["agemm"] - prof["empty"], 0.0) * 1e3
+        a1_fl = 2 * c["batch"] * d[0] * R[0]
+        st_us = t_s * 1e6 / steps
+        a1 = {"a1_gemm_us": round(a1_us, 2), "a1_gemm_mflop": round(a1_fl / 1e6, 1),
+              "a1_gemm_tflops": round(a1_fl / (a1_us * 1e-6) / 1e12, 2) if a1_us > 0 else None,
+              "step_mfma_frac_excl_a1": round((sum(fwd_f) + sum(bwd_f) - a1_fl) /
+                                              ((st_us - a1_us) * 1e-6) / FP32_MFMA_PEAK, 4),
+              "kernel": "hand-written k_agemm (csrc/agemm.hip); no library GEMM in the step"}
     acc = PredictiveLSE(m._engine, Xt, Yt)
     acc.add_sample()
     S = 3 if cfg == 5 else 10
@@ -231,7 +242,8 @@ def bench_config(cfg, dev, rank, world, barrier_sync, max_over_ranks, steps):
            "step_mfma_frac": round((sum(fwd_f) + sum(bwd_f)) / (t_s / steps) / FP32_MFMA_PEAK, 4),
            "predictive_samples_per_s": round(world * S / t_p, 3), "n_test": nt,
            "predictive_kernel_ms": round(k_ms, 3),
-           "predictive_mfma_frac": round(fp / (k_ms * 1e-3) / FP32_MFMA_PEAK, 4)}
+           "predictive_mfma_frac": round(fp / (k_ms * 1e-3) / FP32_MFMA_PEAK, 4),
+           "a1_gemm": a1}
     del m, acc, X, Y, Xt, Yt
     torch.cuda.empty_cache()
     return out

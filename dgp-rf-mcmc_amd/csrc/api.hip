@@ -428,21 +428,28 @@ int dgprf_profile_step(const dgprf_plan_t* plan, const dgprf_chain_t* chain,
   st.grad_only = 0;
   const UpdateDev ud = make_update_dev(st);
   const int L = plan->n_layers, K = 2 * L + 1;
-  hipEvent_t ev[2 * (2 * DGPRF_MAX_LAYERS + 2)] = {};
+  // wide first layer (per-layer forward): its A_1 GEMM is timed in a pair of its own, slot K + 1
+  const bool ag = plan->a0_off >= 0 && !dgprf_sk::step_fused_fwd(*plan);
+  hipEvent_t ev[2 * (2 * DGPRF_MAX_LAYERS + 3)] = {};
   hipError_t e = hipSuccess;
-  for (int i = 0; i < 2 * (K + 1) && e == hipSuccess; ++i) e = hipEventCreate(&ev[i]);
-  for (int k = 0; k <= K; ++k) ms_out[k] = 0.f;
+  for (int i = 0; i < 2 * (K + 2) && e == hipSuccess; ++i) e = hipEventCreate(&ev[i]);
+  for (int k = 0; k <= K + 1; ++k) ms_out[k] = 0.f;
   // the real step sequence (fwd 0..L-1, bwd L-1..0, update), every kernel between two events
   for (int rep = 0; rep < reps && e == hipSuccess; ++rep) {
     const StepDev sd = make_step_dev(*plan, *chain, *batch, st.step_offset);
     e = dgprf::launch_gather(*plan, sd, s);
     for (int j = 0; j < K && e == hipSuccess; ++j) {
       const int kk = j < L ? j : (j < 2 * L ? L + (2 * L - 1 - j) : 2 * L);
-      e = hipEventRecord(ev[2 * kk], s);
+      if (kk == 0 && ag) {
+        e = hipEventRecord(ev[2 * (K + 1)], s);
+        if (e == hipSuccess) e = dgprf::launch_step_agemm(*plan, sd, s);
+        if (e == hipSuccess) e = hipEventRecord(ev[2 * (K + 1) + 1], s);
+      }
+      if (e == hipSuccess) e = hipEventRecord(ev[2 * kk], s);
       if (e != hipSuccess) break;
       if (kk < L && dgprf_sk::step_fused_fwd(*plan))  // one all-layer forward (timed as layer 0)
         e = kk == 0 ? dgprf::launch_step_fwd_fused(*plan, sd, s) : hipSuccess;
-      else if (kk < L) e = dgprf::launch_step_fwd(*plan, sd, kk, s);
+      else if (kk < L) e = dgprf::launch_step_fwd(*plan, sd, kk, s, /*with_agemm=*/!ag);
       else if (kk < 2 * L) e = dgprf::launch_step_bwd(*plan, sd, kk - L, s);
       else e = dgprf::launch_step_update(*plan, sd, ud, nullptr, s);
       if (e == hipSuccess) e = hipEventRecord(ev[2 * kk + 1], s);
@@ -451,13 +458,13 @@ int dgprf_profile_step(const dgprf_plan_t* plan, const dgprf_chain_t* chain,
     if (e == hipSuccess) e = hipEventRecord(ev[2 * K], s);  // empty pair: the pair's own cost
     if (e == hipSuccess) e = hipEventRecord(ev[2 * K + 1], s);
     if (e == hipSuccess) e = hipEventSynchronize(ev[2 * K + 1]);
-    for (int kk = 0; kk <= K && e == hipSuccess; ++kk) {
+    for (int kk = 0; kk <= K + (ag ? 1 : 0) && e == hipSuccess; ++kk) {
       float ms = 0.f;
       e = hipEventElapsedTime(&ms, ev[2 * kk], ev[2 * kk + 1]);
       ms_out[kk] += ms / (float)reps;
     }
   }
-  for (int i = 0; i < 2 * (K + 1); ++i)
+  for (int i = 0; i < 2 * (K + 2); ++i)
     if (ev[i]) (void)hipEventDestroy(ev[i]);
   return hip_rc(e);
 }

@@ -87,7 +87,9 @@ inline void set_lds_limit(const void* fn, size_t bytes) {
 }
 
 // Forward / backward of one layer of the step (k_step_fwd / k_step_bwd).
-hipError_t launch_step_fwd(const dgprf_plan_t& pl, const StepDev& sd, int layer, hipStream_t s);
+// with_agemm = false: layer 0 without its A_1 = X Omega_1 GEMM (timed apart by dgprf_profile_step)
+hipError_t launch_step_fwd(const dgprf_plan_t& pl, const StepDev& sd, int layer, hipStream_t s,
+                           bool with_agemm = true);
 hipError_t launch_step_bwd(const dgprf_plan_t& pl, const StepDev& sd, int layer, hipStream_t s);
 // Large minibatches, one chain (dgprf_sk::step_fused_fwd): the forward of every layer as one
 // launch of the predictive kernel, complete F_l into slice 0 of the F partial buffers.

@@ -659,7 +659,8 @@ hipError_t launch_step_agemm(const dgprf_plan_t& pl, const StepDev& sd, hipStrea
   return hipGetLastError();
 }
 
-hipError_t launch_step_fwd(const dgprf_plan_t& pl, const StepDev& sd, int layer, hipStream_t s) {
+hipError_t launch_step_fwd(const dgprf_plan_t& pl, const StepDev& sd, int layer, hipStream_t s,
+                           bool with_agemm) {
   // 8 waves per workgroup when every wave still gets >= 2 chunks (config 3, cpw = 2: one chunk
   // per wave measured slower, 37.6 vs 35.9 us/step)
   const bool w8 = pl.cpw[layer] >= 4 && pl.cpw[layer] % 2 == 0;
@@ -668,7 +669,7 @@ hipError_t launch_step_fwd(const dgprf_plan_t& pl, const StepDev& sd, int layer,
   const int nwf = (w8 && pl.cpw[layer] % 8 == 0) ? 16 : (w8 ? 8 : 4);
   int lds_floats = 0;
   LayerK a = make_layer_k(pl, sd, layer, lds_floats, false, nwf);
-  if (a.a0) {  // wide first layer: A_1 = X Omega_1 first
+  if (a.a0 && with_agemm) {  // wide first layer: A_1 = X Omega_1 first
     const hipError_t e = launch_step_agemm(pl, sd, s);
     if (e != hipSuccess) return e;
   }

@@ -437,17 +437,18 @@ class Engine:
     def profile_step(self, X_all, Y_all, batch_size, data_size, lr, beta, T, reps=200,
                      perm_seed=0):
         """Average device ms of the event pair around each step kernel (hipEvents,
-        dgprf_profile_step): {'fwd': [L], 'bwd': [L], 'update': float, 'empty': float}, 'empty'
-        being an event pair with no kernel between (the pair's own cost)."""
+        dgprf_profile_step): {'fwd': [L], 'bwd': [L], 'update': float, 'empty': float,
+        'agemm': float}, 'empty' being an event pair with no kernel between (the pair's own cost),
+        'agemm' the A_1 = X Omega_1 GEMM of a wide first layer (0 without one)."""
         pl, ws, bt, keep = self._batch(X_all, Y_all, batch_size, N.BATCH_EPOCH, None, perm_seed)
         ch = self.chain_struct(ws)
         st = self.step_struct(lr, beta, T, data_size)
-        ms = (ctypes.c_float * (2 * self.L + 2))()
+        ms = (ctypes.c_float * (2 * self.L + 3))()
         N.call("dgprf_profile_step", ctypes.byref(pl), ctypes.byref(ch), ctypes.byref(bt),
                ctypes.byref(st), int(reps), ctypes.cast(ms, ctypes.c_void_p), stream())
         v = list(ms)
         return {"fwd": v[:self.L], "bwd": v[self.L:2 * self.L], "update": v[2 * self.L],
-                "empty": v[2 * self.L + 1]}
+                "empty": v[2 * self.L + 1], "agemm": v[2 * self.L + 2]}
 
     # ---------------------------------------------------------------- forward / predictive
     def forward(self, X, Y=None, f_out=False, logp=False, se=False, lse=None, omega=None,

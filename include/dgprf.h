@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define DGPRF_ABI_VERSION 5
+#define DGPRF_ABI_VERSION 6
 
 #define DGPRF_MAX_LAYERS 8
 #define DGPRF_MAX_G 64        /* max latent GPs per layer (n_gp[l]) */
@@ -277,9 +277,11 @@ int dgprf_graph_destroy(dgprf_graph_handle graph);
 
 /* Per-kernel device time of the step sequence, measured with hipEvents on `stream`: `reps` real
  * steps (forward l = 0..L-1, backward L-1..0, update; the chain advances) with an event pair around
- * every kernel.  ms_out[k] (2L + 2 entries) receives the mean milliseconds of the pair around kernel
- * k, indexed forward l -> l, backward l -> L + l, update -> 2L, and ms_out[2L + 1] the mean of an
- * empty pair recorded the same way (the pair's own cost, to subtract). */
+ * every kernel.  ms_out[k] (2L + 3 entries) receives the mean milliseconds of the pair around kernel
+ * k, indexed forward l -> l, backward l -> L + l, update -> 2L, ms_out[2L + 1] the mean of an
+ * empty pair recorded the same way (the pair's own cost, to subtract), and ms_out[2L + 2] the pair
+ * around the A_1 = X Omega_1 GEMM of a wide first layer (0 without one; forward 0 then excludes
+ * it).  ABI 6: the A_1 slot. */
 int dgprf_profile_step(const dgprf_plan_t *plan, const dgprf_chain_t *chain,
                        const dgprf_batch_t *batch, const dgprf_step_t *step, int32_t reps,
                        float *ms_out, void *stream);
