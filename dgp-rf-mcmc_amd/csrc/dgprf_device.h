@@ -46,6 +46,17 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 __device__ __forceinline__ rsrc_t make_rsrc(const float* p, int64_t n_floats) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)(n_floats * 4), 0x00020000);
 }
+// The same, for call sites whose pointer / size the compiler cannot prove wave-uniform (values
+// derived through selects or dynamically indexed kernel-argument arrays): both go through
+// readfirstlane, so the descriptor is built in SGPRs instead of a waterfall loop around every load.
+// Only for values that ARE wave-uniform.
+__device__ __forceinline__ rsrc_t make_rsrc_u(const float* p, int n_floats) {
+  const uint64_t a = (uint64_t)p;
+  const uint64_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  const uint64_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(lo | (hi << 32)), (short)0,
+                                           __builtin_amdgcn_readfirstlane(n_floats * 4), 0x00020000);
+}
 __device__ __forceinline__ f4 bload4(rsrc_t r, uint32_t byte_off) {
   return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
 }

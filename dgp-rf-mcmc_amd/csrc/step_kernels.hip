@@ -177,6 +177,9 @@ __device__ void hyper_block(const UpdK& a, int hb, int chain, float* sm, int sb)
   int l = 0;
   for (int q = 1; q < L; ++q)
     if (hb >= k.b0[q]) l = q;
+  // uniform by construction; through readfirstlane so the partial-row descriptor below is built in
+  // SGPRs (otherwise each of its loads is a waterfall loop)
+  l = __builtin_amdgcn_readfirstlane(l);
   const int j = hb - k.b0[l], d = k.d[l], R = k.R[l], nv = 2 * d + 1, hs = (nv + 3) & ~3;
   const int Q = hs >> 2, ns = k.ns[l], P = a.n_rt * ns, RG = Q >= NT ? 1 : NT / Q;
   const bool kern = (k.flags & DGPRF_HYP_KERNEL) != 0, mean = (k.flags & DGPRF_HYP_MEAN) != 0;
@@ -195,7 +198,7 @@ __device__ void hyper_block(const UpdK& a, int hb, int chain, float* sm, int sb)
   const int64_t n_el = (int64_t)d * R, base = (int64_t)j * HYP_EPB;
   f4 zv[4];
   if (!GONLY) {
-    const rsrc_t rz = make_rsrc(k.z + k.om_off[l], n_el);
+    const rsrc_t rz = make_rsrc_u(k.z + k.om_off[l], (int)n_el);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int64_t i = base + 4 * (tid + NT * u);
@@ -218,7 +221,7 @@ __device__ void hyper_block(const UpdK& a, int hb, int chain, float* sm, int sb)
   // rows p = rt * ns + sl of a row group advance by RG: (rt, sl) tracked without divisions
   constexpr int HYP_U = 8;
   const float* hp = k.ws + (int64_t)chain * a.ws_cs + k.hpp_off[l];
-  const rsrc_t rh = make_rsrc(hp, (int64_t)a.n_rt * NSM * hs);
+  const rsrc_t rh = make_rsrc_u(hp, a.n_rt * NSM * hs);
   const int st_rt = RG / ns, st_sl = RG - st_rt * ns;
   for (int i = tid; i < RG * Q; i += NT) {
     const int q = i % Q, rg = i / Q;
