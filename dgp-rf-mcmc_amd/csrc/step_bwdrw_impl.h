@@ -134,8 +134,11 @@ __global__ __launch_bounds__(64 * NWV) void k_step_bwd_rw(const LayerK a) {
     for (int e = 0; e < EX; ++e) {
       const int k = 4 * e + lq, b = row0 + lr;
       const bool ok = b < row_end && k < d;
-      px[e] = k < a.gp ? bload1(rws, ok ? (uint32_t)((a.fprev_off + b * a.gp + k) * 4) : DGPRF_OOB)
-                       : bload1(rxd, ok ? (uint32_t)((b * (d - a.gp) + (k - a.gp)) * 4) : DGPRF_OOB);
+      // both sources loaded (one OOB-masked to 0) and added: a per-lane choice between the two
+      // descriptors would compile to a waterfall loop around the load
+      const float vf = bload1(rws, ok && k < a.gp ? (uint32_t)((a.fprev_off + b * a.gp + k) * 4) : DGPRF_OOB);
+      const float vd = bload1(rxd, ok && k >= a.gp ? (uint32_t)((b * (d - a.gp) + (k - a.gp)) * 4) : DGPRF_OOB);
+      px[e] = vf + vd;
     }
 #pragma unroll
     for (int e = 0; e < ED; ++e) {
