@@ -129,7 +129,8 @@ hipError_t launch_fresh_omega(const dgprf_plan_t& pl, const StepDev& sd, hipStre
 // scratch query so both size the chunks identically.
 struct ForwardCfg {
   bool wide0, tiles;
-  int rows_waves;  // waves per 16-row tile of the row kernel (4 or 16)
+  int rows_waves;  // waves per workgroup of the row kernel (4, 8 or 16)
+  int rows_tt;     // 16-row tiles per row-kernel workgroup (2: tiles outnumber the CUs)
   int64_t chunk, scratch_floats;
 };
 ForwardCfg forward_cfg(const dgprf_plan_t& pl, int64_t n);

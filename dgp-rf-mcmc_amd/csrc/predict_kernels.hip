@@ -34,7 +34,7 @@ struct FwdLds {
   int xst, ftst, red_off, ft_off, total;
 };
 
-__host__ __device__ inline FwdLds fwd_lds(const dgprf_plan_t& pl, int nwr = NW) {
+__host__ __device__ inline FwdLds fwd_lds(const dgprf_plan_t& pl, int nwr = NW, int tt = 1) {
   int dmax = 4, gmax = 1;
   for (int l = 0; l < pl.n_layers; ++l) {
     dmax = pl.d[l] > dmax ? pl.d[l] : dmax;
@@ -43,11 +43,11 @@ __host__ __device__ inline FwdLds fwd_lds(const dgprf_plan_t& pl, int nwr = NW) 
   FwdLds L;
   L.xst = round4(dmax) + 1;
   L.ftst = round4(gmax) + 1;
-  L.red_off = round4(TR * L.xst);
-  // per-wave F partials [16 rows][16 x output tiles]: sized for the model's widest layer, so the
-  // 8- and 16-wave kernels fit two workgroups per CU
-  L.ft_off = L.red_off + nwr * TR * (((gmax + 15) >> 4) << 4);
-  L.total = L.ft_off + round4(TR * L.ftst);
+  L.red_off = round4(tt * TR * L.xst);
+  // per-wave F partials [tt tiles x 16 rows][16 x output tiles]: sized for the model's widest
+  // layer, so the 8- and 16-wave kernels fit two workgroups per CU
+  L.ft_off = L.red_off + nwr * tt * TR * (((gmax + 15) >> 4) << 4);
+  L.total = L.ft_off + round4(tt * TR * L.ftst);
   return L;
 }
 
@@ -65,7 +65,7 @@ struct FOut {
 // caller): compile-time, so the Omega loads and A-tile MFMAs carry no per-k-step branch (a runtime
 // count put every load and MFMA behind its own branch and wait: ≈2 us per chunk group on config 3);
 // k-steps past d load zeros (out-of-range buffer offsets) against zero x fragments.
-template <bool SMALLD, int NOT, bool RBF, bool G1, int NWR, int NKS>
+template <bool SMALLD, int NOT, bool RBF, bool G1, int NWR, int NKS, int TT = 1>
 __device__ __forceinline__ void layer_partial(const float* __restrict__ om,
                                               const float* __restrict__ W, int R, int d, int g,
                                               float cl, const float* xs, int xst, float* red,
@@ -73,9 +73,14 @@ __device__ __forceinline__ void layer_partial(const float* __restrict__ om,
                                               const float* __restrict__ arow = nullptr) {
   constexpr int CG = NWR >= 16 ? DGPRF_ROWS16_CG : ((NWR >= 8 || NOT > 1) ? 2 : 4);
   static_assert(NKS == 2 || NKS == 3 || NKS == 4 || NKS == 8, "k-step bucket");
-  float xf[NKS];
+  // TT tiles per workgroup (rows t * 16 + lr): every Omega / W fragment serves all of them
+  static_assert(TT == 1 || SMALLD, "two-tile workgroups: register-fragment path only");
+  float xf[TT][NKS];
 #pragma unroll
-  for (int ks = 0; ks < NKS; ++ks) xf[ks] = (SMALLD && 4 * ks < d) ? xs[lr * xst + 4 * ks + lq] : 0.f;
+  for (int t = 0; t < TT; ++t)
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks)
+      xf[t][ks] = (SMALLD && 4 * ks < d) ? xs[(t * TR + lr) * xst + 4 * ks + lq] : 0.f;
   const int nks = (d + 3) >> 2;  // k-steps of the !SMALLD loop
   float omk[CG][NKS], wf[CG][NOT][4][2];
   // buffer loads: 32-bit offsets (one VGPR per address), masked lanes read 0 without traffic
@@ -102,10 +107,14 @@ __device__ __forceinline__ void layer_partial(const float* __restrict__ om,
       }
     }
   };
-  f4 acc[NOT], acs[NOT];
+  f4 acc[TT][NOT], acs[TT][NOT];
+  float dot[TT];
 #pragma unroll
-  for (int ot = 0; ot < NOT; ++ot) acc[ot] = acs[ot] = f4zero();
-  float dot = 0.f;
+  for (int t = 0; t < TT; ++t) {
+    dot[t] = 0.f;
+#pragma unroll
+    for (int ot = 0; ot < NOT; ++ot) acc[t][ot] = acs[t][ot] = f4zero();
+  }
   constexpr int STEP = NWR * 16;
   for (int base = wave * 16; base < R; base += CG * STEP) {
 #pragma unroll
@@ -115,10 +124,12 @@ __device__ __forceinline__ void layer_partial(const float* __restrict__ om,
     for (int j = 0; j < CG; ++j) {
       const int f0 = base + j * STEP;
       if (f0 >= R) break;
+#pragma unroll
+      for (int t = 0; t < TT; ++t) {
       f4 at = f4zero();
       if (SMALLD) {
 #pragma unroll
-        for (int ks = 0; ks < NKS; ++ks) at = mfma16(omk[j][ks], xf[ks], at);
+        for (int ks = 0; ks < NKS; ++ks) at = mfma16(omk[j][ks], xf[t][ks], at);
       } else if (arow) {  // precomputed A row (wide first layer): A[row lr][f0 + 4lq + r]
         at = *reinterpret_cast<const f4*>(arow + f0 + 4 * lq);
       } else {
@@ -145,32 +156,38 @@ __device__ __forceinline__ void layer_partial(const float* __restrict__ om,
       if (G1) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          dot = fmaf(p0[r], wf[j][0][r][0], dot);
-          if (RBF) dot = fmaf(p1[r], wf[j][0][r][1], dot);
+          dot[t] = fmaf(p0[r], wf[j][0][r][0], dot[t]);
+          if (RBF) dot[t] = fmaf(p1[r], wf[j][0][r][1], dot[t]);
         }
       } else {
 #pragma unroll
         for (int ot = 0; ot < NOT; ++ot)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            acc[ot] = mfma16(wf[j][ot][r][0], p0[r], acc[ot]);
-            if (RBF) acs[ot] = mfma16(wf[j][ot][r][1], p1[r], acs[ot]);
+            acc[t][ot] = mfma16(wf[j][ot][r][0], p0[r], acc[t][ot]);
+            if (RBF) acs[t][ot] = mfma16(wf[j][ot][r][1], p1[r], acs[t][ot]);
           }
+      }
       }
     }
   }
   constexpr int GP = NOT * 16;
-  float* redw = red + wave * TR * GP;
-  if (G1) {
-    dot += __shfl_xor(dot, 16);
-    dot += __shfl_xor(dot, 32);
-    if (lq == 0) redw[lr * GP] = dot;
-  } else {
-    // acc[ot][r] = F partial[row lr][ot*16 + 4lq + r]
+  float* redw = red + wave * TT * TR * GP;
 #pragma unroll
-    for (int ot = 0; ot < NOT; ++ot)
+  for (int t = 0; t < TT; ++t) {
+    float* rt = redw + t * TR * GP;
+    if (G1) {
+      float v = dot[t];
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      if (lq == 0) rt[lr * GP] = v;
+    } else {
+      // acc[t][ot][r] = F partial[tile t, row lr][ot*16 + 4lq + r]
 #pragma unroll
-      for (int r = 0; r < 4; ++r) redw[lr * GP + ot * 16 + 4 * lq + r] = acc[ot][r] + acs[ot][r];
+      for (int ot = 0; ot < NOT; ++ot)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) rt[lr * GP + ot * 16 + 4 * lq + r] = acc[t][ot][r] + acs[t][ot][r];
+    }
   }
 }
 
@@ -179,9 +196,16 @@ __device__ __forceinline__ void layer_partial(const float* __restrict__ om,
 // per SIMD) for test sets too small to fill the chip with the one-wave-per-tile tile kernel.
 // NWR = 8 / 16 are budgeted for two workgroups per CU (4 / 8 waves per SIMD): with one, a test set
 // of more tiles than CUs (config 3: 286) runs in two rounds.
-template <bool SMALLD, int NOTMAX, int NWR>
+// TT = 2: two 16-row tiles per workgroup (16 waves, one workgroup per CU), every W / Omega
+// fragment a wave loads serves both tiles — the choice once the tiles outnumber the CUs, where a CU
+// has to run two tiles anyway and two one-tile workgroups would each fetch the whole model.
+// WPE: waves per SIMD the registers are budgeted for — 8 for 16-wave workgroups that may share a
+// CU (explicit DGPRF_FWD_ROWS16 past one tile per CU), 4 when each CU holds one workgroup (the
+// 16-wave kernel then keeps its fragments in registers instead of spilling).
+template <bool SMALLD, int NOTMAX, int NWR, int TT = 1,
+          int WPE = (NWR == 16 ? DGPRF_ROWS16_WPE : (NWR == 8 ? 4 : 1))>
 __global__ __launch_bounds__(64 * NWR)
-__attribute__((amdgpu_waves_per_eu(NWR == 16 ? DGPRF_ROWS16_WPE : (NWR == 8 ? 4 : 1))))
+__attribute__((amdgpu_waves_per_eu(TT > 1 ? 4 : WPE)))
 void k_forward_rows(
     const dgprf_plan_t pl, const float* __restrict__ theta, const float* __restrict__ omega,
     const float* __restrict__ der, const float* __restrict__ X, const float* __restrict__ Y,
@@ -192,12 +216,12 @@ void k_forward_rows(
   // rows [row_begin, row_end) of the n-row set; a0 = A_1 = X Omega_1 of those rows
   // ([row - row_begin][R_1], k_step_agemm) for a wide first layer, or nullptr
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const FwdLds LD = fwd_lds(pl, NWR);
+  const FwdLds LD = fwd_lds(pl, NWR, TT);
   const int chain = blockIdx.y;
   const int64_t ochain = pl.hyp_per_chain ? (int64_t)chain * pl.omega_total : 0;
   const int64_t dchain = pl.hyp_per_chain ? (int64_t)chain * pl.der_total : 0;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, lr = lane & 15, lq = lane >> 4;
-  const int64_t row0 = row_begin + (int64_t)blockIdx.x * TR;
+  const int64_t row0 = row_begin + (int64_t)blockIdx.x * TR * TT;
   float* xs = smem;
   float* red = smem + LD.red_off;
   float* ft = smem + LD.ft_off;
@@ -209,7 +233,7 @@ void k_forward_rows(
     const int R = pl.n_rf[layer], g = pl.n_gp[layer];
     const int gp = layer > 0 ? pl.n_gp[layer - 1] : 0;
     const float* arow = (layer == 0 && a0) ? a0 + (row0 - row_begin + lr) * (int64_t)R : nullptr;
-    for (int e = threadIdx.x; !arow && e < TR * dpad; e += blockDim.x) {
+    for (int e = threadIdx.x; !arow && e < TT * TR * dpad; e += blockDim.x) {
       const int r = e / dpad, k = e - r * dpad;
       const int64_t b = row0 + r;
       float v = 0.f;
@@ -229,13 +253,13 @@ void k_forward_rows(
 #define DGPRF_LP(SD, NT, RB, G1_)                                                               \
   do {                                                                                          \
     if (!SD || d > 16)                                                                          \
-      layer_partial<SD, NT, RB, G1_, NWR, 8>(om, W, R, d, g, cl, xs, LD.xst, red, wave, lr, lq, arow); \
+      layer_partial<SD, NT, RB, G1_, NWR, 8, TT>(om, W, R, d, g, cl, xs, LD.xst, red, wave, lr, lq, arow); \
     else if (d > 12)                                                                            \
-      layer_partial<SD, NT, RB, G1_, NWR, 4>(om, W, R, d, g, cl, xs, LD.xst, red, wave, lr, lq, arow); \
+      layer_partial<SD, NT, RB, G1_, NWR, 4, TT>(om, W, R, d, g, cl, xs, LD.xst, red, wave, lr, lq, arow); \
     else if (d > 8)                                                                             \
-      layer_partial<SD, NT, RB, G1_, NWR, 3>(om, W, R, d, g, cl, xs, LD.xst, red, wave, lr, lq, arow); \
+      layer_partial<SD, NT, RB, G1_, NWR, 3, TT>(om, W, R, d, g, cl, xs, LD.xst, red, wave, lr, lq, arow); \
     else                                                                                        \
-      layer_partial<SD, NT, RB, G1_, NWR, 2>(om, W, R, d, g, cl, xs, LD.xst, red, wave, lr, lq, arow); \
+      layer_partial<SD, NT, RB, G1_, NWR, 2, TT>(om, W, R, d, g, cl, xs, LD.xst, red, wave, lr, lq, arow); \
   } while (0)
 #define DGPRF_LP_ALL(SD)                                                                        \
   do {                                                                                          \
@@ -256,19 +280,23 @@ void k_forward_rows(
       else DGPRF_LP(SD, (NOTMAX >= 4 ? 4 : 1), false, false);                                   \
     }                                                                                           \
   } while (0)
-      if (SMALLD || d <= 32) DGPRF_LP_ALL(true);
-      else DGPRF_LP_ALL(false);
+      if constexpr (TT > 1) {  // host-selected for d <= 32 models only
+        DGPRF_LP_ALL(true);
+      } else {
+        if (SMALLD || d <= 32) DGPRF_LP_ALL(true);
+        else DGPRF_LP_ALL(false);
+      }
 #undef DGPRF_LP_ALL
 #undef DGPRF_LP
     }
     const int GP = ((g + 15) >> 4) * 16;
     __syncthreads();
     float* out = fo.p[layer] ? fo.p[layer] + (int64_t)chain * n * g : nullptr;
-    for (int e = threadIdx.x; e < TR * g; e += blockDim.x) {
+    for (int e = threadIdx.x; e < TT * TR * g; e += blockDim.x) {
       const int r = e / g, o = e - r * g;
       float v = red[r * GP + o];
 #pragma unroll
-      for (int w = 1; w < NWR; ++w) v += red[w * TR * GP + r * GP + o];
+      for (int w = 1; w < NWR; ++w) v += red[w * TT * TR * GP + r * GP + o];
       ft[r * LD.ftst + o] = v;
       const int64_t b = row0 + r;
       if (out && b < row_end) out[b * g + o] = v;
@@ -278,7 +306,7 @@ void k_forward_rows(
 
   // likelihood per row (threads 0..15)
   const bool want_lik = logp_out || se_out || lse_m;
-  if (want_lik && threadIdx.x < TR) {
+  if (want_lik && threadIdx.x < TT * TR) {
     const int64_t b = row0 + threadIdx.x;
     if (b < row_end) {
       const int g = pl.n_gp[L - 1];
@@ -1021,6 +1049,14 @@ ForwardCfg forward_cfg(const dgprf_plan_t& pl, int64_t n) {
       c.rows_waves = few && small ? ((n + TR - 1) / TR > device_cus() ? 8 : 16) : 4;
       break;
   }
+  // past one tile per CU a CU runs two tiles anyway: one 16-wave workgroup over two tiles fetches
+  // each W / Omega fragment once for both (instead of two 8-wave workgroups fetching the model
+  // twice).  DGPRF_FWD_ROWS8 keeps the two-workgroup form.
+  c.rows_tt = 1;
+  if (pl.fwd_path == DGPRF_FWD_AUTO && c.rows_waves == 8 && !c.wide0 && !getenv("DGPRF_ROWS_TT1")) {
+    c.rows_waves = 16;
+    c.rows_tt = 2;
+  }
   // chunks are whole 64-row tile-kernel workgroups: every wave of the last workgroup reads its 16
   // A_1 rows (rows past n included, their outputs discarded), so the scratch covers align64 rows
   const int64_t R0 = pl.n_rf[0];
@@ -1102,9 +1138,9 @@ hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const
 #undef DGPRF_TILE_LAUNCH
 #undef DGPRF_TILE_LAUNCH1
     } else {
-      const int nwr = cfg.rows_waves;
-      const size_t lds = (size_t)fwd_lds(pl, nwr).total * sizeof(float);
-      dim3 grid((unsigned)((nr + TR - 1) / TR), pl.n_chains);
+      const int nwr = cfg.rows_waves, tt = cfg.rows_tt;
+      const size_t lds = (size_t)fwd_lds(pl, nwr, tt).total * sizeof(float);
+      dim3 grid((unsigned)((nr + TR * tt - 1) / (TR * tt)), pl.n_chains);
 #define DGPRF_FWD_LAUNCH_W(S, NM, NWR_)                                                             \
   do {                                                                                             \
     set_lds_limit((const void*)k_forward_rows<S, NM, NWR_>, lds);                                  \
@@ -1112,7 +1148,16 @@ hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const
                        omega, der, X, Y, y_cols, n, fo, logp, se, lse_m, lse_s, se_sum, a0, r0, r1); \
   } while (0)
 #define DGPRF_FWD_LAUNCH(S, NM) DGPRF_FWD_LAUNCH_W(S, NM, 4)
-      if (smalld && nwr == 16) {  // g <= 16 (forward_cfg)
+      if (smalld && tt == 2) {  // g <= 16, no wide first layer (forward_cfg)
+        set_lds_limit((const void*)k_forward_rows<true, 1, 16, 2>, lds);
+        hipLaunchKernelGGL((k_forward_rows<true, 1, 16, 2>), grid, dim3(64 * 16), lds, s, pl, theta,
+                           omega, der, X, Y, y_cols, n, fo, logp, se, lse_m, lse_s, se_sum, a0, r0, r1);
+      } else if (smalld && nwr == 16 && (nr + TR - 1) / TR <= device_cus() &&
+                 !getenv("DGPRF_ROWS16_WPE8")) {  // one workgroup per CU: 4 waves per SIMD
+        set_lds_limit((const void*)k_forward_rows<true, 1, 16, 1, 4>, lds);
+        hipLaunchKernelGGL((k_forward_rows<true, 1, 16, 1, 4>), grid, dim3(64 * 16), lds, s, pl, theta,
+                           omega, der, X, Y, y_cols, n, fo, logp, se, lse_m, lse_s, se_sum, a0, r0, r1);
+      } else if (smalld && nwr == 16) {  // g <= 16 (forward_cfg)
         DGPRF_FWD_LAUNCH_W(true, 1, 16);
       } else if (smalld && nwr == 8) {
         DGPRF_FWD_LAUNCH_W(true, 1, 8);

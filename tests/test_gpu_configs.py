@@ -113,6 +113,24 @@ def test_predictive_paths_small_test_set(dev, path, cfg):
     assert np.max(np.abs(lp - ref)) < 2e-5 * max(1.0, np.max(np.abs(ref)))
 
 
+@pytest.mark.parametrize("cfg,n", [(3, 4573), (2, 5001)])
+def test_predictive_two_tile_rows(dev, cfg, n):
+    """The default path once the 16-row tiles outnumber the CUs (config 3's 4,573 test rows: 286
+    tiles): the row kernel with two tiles per 16-wave workgroup (forward_cfg rows_tt = 2), whose
+    last workgroup holds a ragged tile (and for 5,001 rows an empty one); per-row log p against the
+    oracle, and identical to the one-tile 8-wave workgroups to fp32 rounding."""
+    from dgprf import _native as N
+    c = CONFIGS[cfg]
+    m, p = _model(c, 35)
+    Xt, Yt = _data(c, n, 205)
+    lp = cpu(m._engine.forward(Xt, Yt, logp=True)["logp"][0])
+    ref = O.log_prob(p, O.forward(p, Xt), Yt)
+    assert np.max(np.abs(lp - ref)) < 2e-5 * max(1.0, np.max(np.abs(ref)))
+    m._engine.set_forward_path(N.FWD_ROWS8)
+    lp8 = cpu(m._engine.forward(Xt, Yt, logp=True)["logp"][0])
+    assert np.max(np.abs(lp - lp8)) < 2e-5 * max(1.0, np.max(np.abs(ref)))
+
+
 def test_predictive_multi_round_rows(dev):
     """Config 2's shape (3-layer RBF, n_rf 1024, g [8,8,1]) over 70,001 test rows: more tiles than
     one round of resident waves (65,536 rows on 256 CUs) plus a ragged remainder; per-row log p
