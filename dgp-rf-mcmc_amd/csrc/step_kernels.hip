@@ -388,6 +388,18 @@ __global__ __launch_bounds__(UPD_THREADS) void k_step_update(const UpdK a) {
   const int e0 = 4 * (bx * UPD_THREADS + (int)threadIdx.x);
   const uint32_t off = (uint32_t)e0 * 4u;
   const int64_t cw = (int64_t)chain * a.w_total;
+  int layer = 0;
+#pragma unroll
+  for (int l = 1; l < DGPRF_MAX_LAYERS; ++l)
+    if (l < a.n_layers && e0 >= a.lo[l]) layer = l;
+  // the mass and the step counter (written by the previous graph's k_advance) are loaded together
+  // with the parameters and partials: placed after the partial sums, the compiler issued them
+  // only once those had been waited for — a second dependent memory round trip per step
+  // layer padding between align4 offsets stays untouched: live elements of the quad (a.hi is
+  // indexed per lane, so this too is a memory load: issued here, not after the sums)
+  const int nlive = min(max(a.hi[layer] - e0, 0), 4);
+  const float M = GONLY ? 1.f : a.mass[chain * a.n_layers + layer];
+  const int64_t t = GONLY ? 0 : *a.step + (int64_t)a.step_offset;
   const rsrc_t rth = make_rsrc(a.theta + cw, a.w_total);
   const f4 th = bload4(rth, off);
   f4 m = f4zero(), gr;
@@ -407,12 +419,6 @@ __global__ __launch_bounds__(UPD_THREADS) void k_step_update(const UpdK a) {
     }
     gr = sacc;
   }
-  int layer = 0;
-#pragma unroll
-  for (int l = 1; l < DGPRF_MAX_LAYERS; ++l)
-    if (l < a.n_layers && e0 >= a.lo[l]) layer = l;
-  // layer padding between align4 offsets stays untouched: live elements of the quad
-  const int nlive = min(max(a.hi[layer] - e0, 0), 4);
   auto store = [&](float* p, f4 v) {
     if (nlive == 4) {
       st4(p, v);
@@ -428,10 +434,6 @@ __global__ __launch_bounds__(UPD_THREADS) void k_step_update(const UpdK a) {
     store(a.grad_out + (int64_t)chain * a.grad_cs + e0, gr);
     return;
   }
-  const float M = a.mass[chain * a.n_layers + layer];
-  // the step counter (written by the previous step's k_advance) is read only now, after the
-  // parameter and partial loads are in flight
-  const int64_t t = *a.step + (int64_t)a.step_offset;
   float lr, T;
   int resample;
   step_schedule<CYC>(ud, t, &lr, &T, &resample);
