@@ -10,7 +10,9 @@ posterior sample + log p + se + the online log-sum-exp accumulation (utils_train
   python bench.py [--gpus N --steps K --warmup W]
   python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
       --master-port P bench.py --gpus N --steps K --warmup W
-Rank 0 prints ONE JSON line.
+Rank 0 prints ONE JSON line.  `--gpus N` is authoritative: without a launcher (WORLD_SIZE unset)
+and N > 1 the process starts the N ranks itself (torch.distributed.run as a child, before any GPU
+call) and exits with its status; under a launcher WORLD_SIZE must equal N.
 """
 import argparse
 import json
@@ -35,7 +37,7 @@ HBM_PEAK = 8.0e12           # MI355X_MICROARCH.md: HBM3E spec (B/s)
 # MI355X_MICROARCH.md per-instruction table: v_sin_f32 / v_cos_f32 issue 8 cycles per 64-lane wave
 # instruction on a SIMD; 256 CUs x 4 SIMDs at the 2.4 GHz peak clock
 TRANS_PER_S = 1024 * 64 / 8 * 2.4e9
-PROFILES = os.path.join(ROOT, "profiles", "r03")   # this round's committed rocprofv3 evidence
+PROFILES = os.path.join(ROOT, "profiles", "r04")   # this round's committed rocprofv3 evidence
 
 CFG = dict(L=3, n_rf=1024, n_gp=[8, 8, 1], D=8, N=1_000_000, B=200, N_test=100_000,
            variance=0.1, lr=0.01, beta=0.9, T=1.0)
@@ -143,7 +145,7 @@ def _short(name):
 
 def pmc_traffic(prefix):
     """HBM-side bytes per launch of the kernels named `prefix...` (dispatch-weighted mean), from the
-    committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes (profiles/r03/pmc_traffic.json, made by
+    committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes (profiles/r04/pmc_traffic.json, made by
     scripts/gpu_profile_round.sh; FETCH doubled per MI355X_MICROARCH.md §HBM).  None if absent."""
     path = os.path.join(PROFILES, "pmc_traffic.json")
     if not os.path.exists(path):
@@ -157,7 +159,7 @@ def pmc_traffic(prefix):
 
 def rocprof_avg_us(prefix, fname="kernel_stats_bench.csv"):
     """Dispatch-weighted average duration (us) of the kernels named `prefix<...>` in the committed
-    rocprofv3 --kernel-trace --stats summary of this bench (profiles/r03/kernel_stats_bench.csv);
+    rocprofv3 --kernel-trace --stats summary of this bench (profiles/r04/kernel_stats_bench.csv);
     None if absent.  Traced durations include each dispatch's own launch overhead."""
     import csv
     path = os.path.join(PROFILES, fname)
@@ -306,6 +308,39 @@ def b_sweep(model, X, Y, N_, batches, d, R, P, g):
     return out
 
 
+def resolve_world(gpus, env, backend, device_count):
+    """What this process does for `--gpus gpus`: ("run", world) — be one rank of `world` — or
+    ("spawn", gpus) — start `gpus` ranks as children.  Raises SystemExit (non-zero) when the
+    launcher's WORLD_SIZE disagrees with --gpus, or when nccl (RCCL, one GPU per rank) is asked for
+    more ranks than visible GPUs.  `device_count` is a callable (torch.cuda.device_count does not
+    initialise the GPU on this image)."""
+    if gpus < 1:
+        raise SystemExit(f"bench.py: --gpus must be >= 1, got {gpus}")
+    ws = env.get("WORLD_SIZE")
+    if ws is not None and int(ws) != gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={ws} from the launcher but --gpus {gpus}")
+    if backend == "nccl" and gpus > 1 and device_count() < gpus:
+        raise SystemExit(f"bench.py: --gpus {gpus} with the nccl backend (one GPU per rank) but "
+                         f"only {device_count()} GPU(s) visible")
+    if ws is None and gpus > 1:
+        return "spawn", gpus
+    return "run", int(ws) if ws is not None else 1
+
+
+def spawn_ranks(gpus, argv):
+    """Run this script as `gpus` ranks under torch.distributed.run (127.0.0.1, a free port) and
+    return its exit status; rank 0 prints the JSON line on the inherited stdout."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={gpus}", "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__)] + list(argv)
+    return subprocess.call(cmd)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -323,12 +358,14 @@ def main():
     ap.add_argument("--b-sweep", type=int, default=1)
     args = ap.parse_args()
 
-    rank = int(os.environ.get("RANK", 0))
-    world = int(os.environ.get("WORLD_SIZE", 1))
-    local = int(os.environ.get("LOCAL_RANK", 0))
     # DGPRF_BENCH_BACKEND=gloo (with ranks sharing a GPU: local % device_count) rehearses the N > 1
     # path on a one-GPU box; the driver's multi-GPU runs use nccl (= RCCL), one GPU per rank
     backend = os.environ.get("DGPRF_BENCH_BACKEND", "nccl")
+    what, world = resolve_world(args.gpus, os.environ, backend, torch.cuda.device_count)
+    if what == "spawn":
+        sys.exit(spawn_ranks(world, sys.argv[1:]))
+    rank = int(os.environ.get("RANK", 0))
+    local = int(os.environ.get("LOCAL_RANK", 0))
     local = local % max(1, torch.cuda.device_count()) if backend == "gloo" else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -436,30 +473,31 @@ def main():
     upd_bytes = 4 * pl.w_total * (pl.n_row_tiles + 2 + 2 + 2)  # gW partials + theta/mom r/w
     dom = max(per_name, key=lambda k: per_name[k][0] * per_name[k][2])
     ms_dom, fl_dom, _ = per_name[dom]
-    # duration per launch: the committed rocprofv3 kernel trace of this bench when present (so
-    # frac recomputes from profiles/r03/), the live event measurement beside it
+    # duration per launch: this run's hipEvent measurement (`achieved` / `frac`); the committed
+    # rocprofv3 kernel trace of the same command (profiles/r04/) beside it as the cross-check
     rp_us = rocprof_avg_us(dom)
-    use_us = rp_us if rp_us else ms_dom * 1e3
+    use_us = ms_dom * 1e3
     n_launch = 2 * len(d) + 1
     bnd_us = launch_boundary_us(dev)
+    rel = os.path.relpath(PROFILES, ROOT)
     roof = {"kernel": dom, "bound": "mfma",
             "achieved": round(fl_dom / (use_us * 1e-6) / 1e12, 6),
             "peak": FP32_MFMA_PEAK / 1e12, "unit": "TFLOP/s",
             "frac": round(fl_dom / (use_us * 1e-6) / FP32_MFMA_PEAK, 8),
             "traffic": pmc_traffic(dom),
-            "traffic_source": "profiles/r03/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE "
+            "traffic_source": f"{rel}/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE "
                               "passes of this bench; bytes per launch incl. Infinity-Cache hits)",
             "avg_launch_us": round(use_us, 3),
-            "duration_source": ("profiles/r03/kernel_stats_bench.csv: rocprofv3 --kernel-trace --stats "
-                                "of this bench, dispatch-weighted average of the kernel's instances"
-                                if rp_us else "live hipEvent measurement (no committed trace found)"),
+            "duration_source": "live: hipEvent pair around the kernel on its launch stream minus an "
+                               "empty pair (dgprf_profile_step, --profile-reps real steps), "
+                               "averaged over the kernel's L launches per step: the in-kernel span",
             "flops_per_launch": int(fl_dom),
-            "live_event_us": round(ms_dom * 1e3, 3),
-            "live_frac": round(fl_dom / (ms_dom * 1e-3) / FP32_MFMA_PEAK, 8),
-            "live_method": "hipEvent pair around the kernel on its launch stream minus an empty "
-                           "pair (dgprf_profile_step, 200 steps): the in-kernel span; the traced "
-                           "duration also holds the dispatch's launch and the tracer's completion "
-                           "signal (DESIGN.md §5)",
+            "rocprof_avg_launch_us": rp_us,
+            "rocprof_frac": (round(fl_dom / (rp_us * 1e-6) / FP32_MFMA_PEAK, 8) if rp_us else None),
+            "rocprof_source": (f"{rel}/kernel_stats_bench.csv: rocprofv3 --kernel-trace --stats of "
+                               "this bench, dispatch-weighted average of the kernel's instances; a "
+                               "traced duration also holds the dispatch's launch and the tracer's "
+                               "completion signal (DESIGN.md §5)" if rp_us else None),
             "launch_floor": {"launches_per_step": n_launch, "boundary_us": round(bnd_us, 3),
                              "floor_us_per_step": round(n_launch * bnd_us, 3),
                              "steps_per_s_ceiling": round(1e6 / (n_launch * bnd_us), 1),

@@ -166,7 +166,7 @@ int dgprf_plan_init(dgprf_plan_t* pl) {
   if (pl->d_in < 1 || pl->d_out < 1 || pl->batch < 1 || pl->n_chains < 1) return DGPRF_E_SHAPE;
   if (pl->likelihood != DGPRF_LIK_GAUSSIAN && pl->likelihood != DGPRF_LIK_SOFTMAX) return DGPRF_E_ARG;
   if (pl->fwd_path < DGPRF_FWD_AUTO || pl->fwd_path > DGPRF_FWD_ROWS8 || pl->agemm_chunk_rows < 0 ||
-      pl->fresh_z < 0 || (pl->fresh_z >> L) != 0)
+      pl->fresh_z < 0 || (pl->fresh_z >> L) != 0 || (pl->bwd_tiles != 0 && pl->bwd_tiles != 1))
     return DGPRF_E_ARG;
   for (int l = 0; l < L; ++l) {
     if (pl->kind[l] != DGPRF_RBF && pl->kind[l] != DGPRF_ARC) return DGPRF_E_ARG;
@@ -239,7 +239,7 @@ int dgprf_plan_init(dgprf_plan_t* pl) {
   pl->rt_per_group = 1;
   pl->rg_full_bayes = 0;
   pl->pad1 = 0;
-  if (pl->n_row_tiles > 16) {
+  if (pl->n_row_tiles > 16 && !pl->bwd_tiles) {
     bool ok = true, ok_fb = true;
     dgprf_sk::RgCfg c;
     for (int l = 0; l < L; ++l) {
@@ -253,6 +253,8 @@ int dgprf_plan_init(dgprf_plan_t* pl) {
   }
   pl->n_gw_rows = (pl->n_row_tiles + pl->rt_per_group - 1) / pl->rt_per_group;
   pl->n_rt_pad = (pl->n_gw_rows + 15) / 16 * 16;
+  // the update kernel addresses the gW partials with 32-bit buffer offsets
+  if ((int64_t)pl->n_rt_pad * pl->w_total >= ((int64_t)1 << 29)) return DGPRF_E_SHAPE;
   pl->gwp_off = ws;
   ws = align4(ws + (int64_t)pl->n_rt_pad * pl->w_total);
   pl->logp_off = ws;
@@ -358,17 +360,6 @@ int dgprf_graph_create_sghmc(dgprf_graph_handle* out, const dgprf_plan_t* plan,
   if (step->full_bayes && plan->fresh_z) return DGPRF_E_ARG;
   hipStream_t cs;
   if (hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess) return DGPRF_E_HIP;
-  if (plan->a0_off >= 0 && getenv("DGPRF_AGEMM") && getenv("DGPRF_AGEMM")[0] == 'l') {
-    // hipBLASLt comparison arm only: library GEMM state (handle, tuned algorithm) before capture
-    // The warm-up writes the workspace's A_1 on `cs`, which is not ordered after the caller's
-    // stream: let every earlier kernel (e.g. gradients still reading A_1) finish first.
-    const StepDev sd0 = make_step_dev(*plan, *chain, *batch, step->step_offset);
-    if (hipDeviceSynchronize() != hipSuccess || dgprf::launch_step_agemm(*plan, sd0, cs) != hipSuccess ||
-        hipStreamSynchronize(cs) != hipSuccess) {
-      (void)hipStreamDestroy(cs);
-      return DGPRF_E_HIP;
-    }
-  }
   hipError_t e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
   dgprf_step_t st = *step;
   st.grad_only = 0;
@@ -523,6 +514,12 @@ int dgprf_gp_matmul(const float* phi, int64_t n, int32_t P, const float* W, int3
                     void* stream) {
   if (n < 0 || P < 1 || g < 1 || !W || (n > 0 && (!phi || !F))) return DGPRF_E_ARG;
   return hip_rc(dgprf::launch_gp_matmul(phi, n, P, W, g, F, as_stream(stream)));
+}
+
+int dgprf_rf_project(const float* X, int64_t n, int32_t ldx, int32_t d, const float* omega,
+                     int32_t R, float* A, void* stream) {
+  if (n < 0 || d < 1 || R < 1 || ldx < d || !omega || (n > 0 && (!X || !A))) return DGPRF_E_ARG;
+  return hip_rc(dgprf::launch_agemm(X, n, ldx, d, omega, R, A, as_stream(stream)));
 }
 
 int dgprf_prior_w(const dgprf_plan_t* plan, const float* theta, float* out, void* stream) {

@@ -107,8 +107,7 @@ hipError_t launch_gather(const dgprf_plan_t& pl, const StepDev& sd, hipStream_t 
 hipError_t launch_agemm(const float* X, int64_t n, int ld, int d, const float* om, int R,
                         float* aout, hipStream_t s);
 hipError_t launch_advance(int64_t* step, int64_t by, hipStream_t s);
-// The step's A_1 GEMM alone (plan.a0_off >= 0); dgprf_graph_create_sghmc runs it once before
-// capture so the GEMM's library handle and algorithm exist when the step is captured.
+// The step's A_1 GEMM alone (plan.a0_off >= 0): the hand-written MFMA kernel of agemm.hip.
 hipError_t launch_step_agemm(const dgprf_plan_t& pl, const StepDev& sd, hipStream_t s);
 // The hand-written MFMA A_1 GEMM (agemm.hip): A[n_out][R] = X[n][d] Omega[d][R] (rows >= n
 // zero) for `batch` chains (element strides sx, so, sa; so = 0: shared Omega).  false: shape
@@ -116,12 +115,9 @@ hipError_t launch_step_agemm(const dgprf_plan_t& pl, const StepDev& sd, hipStrea
 bool own_agemm(const float* X, int64_t n, int64_t n_out, int ldx, int d, const float* om, int R,
                float* aout, int batch, int64_t sx, int64_t so, int64_t sa, hipStream_t s,
                hipError_t* err);
-// hipBLASLt fp32 A = X Omega (row-major, A row stride R) for `batch` chains (element strides sx,
-// so, sa; so = 0: shared Omega).  false: no library path for the shape (caller uses its kernel).
-bool blas_agemm(const float* X, int64_t n, int ldx, int d, const float* om, int R, float* aout,
-                int batch, int64_t sx, int64_t so, int64_t sa, hipStream_t s);
 // plan.fresh_z: Omega of every layer into the workspace (omf_off), fresh layers from Philox z of
-// step *step + step_offset, the others copied from the chain's Omega
+// step *step + step_offset, the others copied from the chain's Omega when the all-layer fused
+// forward reads this copy (per-layer kernels read a fixed layer's Omega in place)
 hipError_t launch_fresh_omega(const dgprf_plan_t& pl, const StepDev& sd, hipStream_t s);
 
 // How dgprf_forward covers n rows: tile or row kernel, the A_1 GEMM for a wide first layer (in

@@ -1053,7 +1053,7 @@ ForwardCfg forward_cfg(const dgprf_plan_t& pl, int64_t n) {
   // each W / Omega fragment once for both (instead of two 8-wave workgroups fetching the model
   // twice).  DGPRF_FWD_ROWS8 keeps the two-workgroup form.
   c.rows_tt = 1;
-  if (pl.fwd_path == DGPRF_FWD_AUTO && c.rows_waves == 8 && !c.wide0 && !getenv("DGPRF_ROWS_TT1")) {
+  if (pl.fwd_path == DGPRF_FWD_AUTO && c.rows_waves == 8 && !c.wide0) {
     c.rows_waves = 16;
     c.rows_tt = 2;
   }
@@ -1152,8 +1152,7 @@ hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const
         set_lds_limit((const void*)k_forward_rows<true, 1, 16, 2>, lds);
         hipLaunchKernelGGL((k_forward_rows<true, 1, 16, 2>), grid, dim3(64 * 16), lds, s, pl, theta,
                            omega, der, X, Y, y_cols, n, fo, logp, se, lse_m, lse_s, se_sum, a0, r0, r1);
-      } else if (smalld && nwr == 16 && (nr + TR - 1) / TR <= device_cus() &&
-                 !getenv("DGPRF_ROWS16_WPE8")) {  // one workgroup per CU: 4 waves per SIMD
+      } else if (smalld && nwr == 16 && (nr + TR - 1) / TR <= device_cus()) {  // one workgroup per CU: 4 waves per SIMD
         set_lds_limit((const void*)k_forward_rows<true, 1, 16, 1, 4>, lds);
         hipLaunchKernelGGL((k_forward_rows<true, 1, 16, 1, 4>), grid, dim3(64 * 16), lds, s, pl, theta,
                            omega, der, X, Y, y_cols, n, fo, logp, se, lse_m, lse_s, se_sum, a0, r0, r1);

@@ -218,7 +218,7 @@ __global__ __launch_bounds__(64 * RG_WAVES) void k_step_bwd_rg(const LayerK a) {
   const int wave0 = __builtin_amdgcn_readfirstlane(t & ~63);
   Elem e0;  // one prologue element per thread (rg_fast: total <= 1024)
   e0.dst = -1;
-  if (a.rg_fast && wave0 < total && !(a.dbg & 1)) rg_issue(a, chain, rt0 * TR, row_end, rows, nx, t, e0);
+  if (a.rg_fast && wave0 < total) rg_issue(a, chain, rt0 * TR, row_end, rows, nx, t, e0);
   RG_STAMP(stamp_base, 1);
   float* dxp = a.dxout + (int64_t)chain * a.ws_cs + (int64_t)sl * B * dxw;
   const float* a0b = KS == 0 && a.a0 ? a.a0 + (int64_t)chain * a.ws_cs : nullptr;
@@ -281,7 +281,7 @@ __global__ __launch_bounds__(64 * RG_WAVES) void k_step_bwd_rg(const LayerK a) {
     }
     // next super tile's partial sums: loads in flight while this one computes
     if (a.rg_fast && it + 1 < n_iter && wave0 < total)
-      if (!(a.dbg & 1)) rg_issue(a, chain, row0 + rows, row_end, rows, nx, t, e0);
+      rg_issue(a, chain, row0 + rows, row_end, rows, nx, t, e0);
     // ---- this wave's row tile rw of the super tile
     const float* xw = xs + rw * TR * a.xst;
     const float* dw = dfs + rw * TR * a.auxst;
@@ -312,7 +312,7 @@ __global__ __launch_bounds__(64 * RG_WAVES) void k_step_bwd_rg(const LayerK a) {
     f4 dxa[4] = {f4zero(), f4zero(), f4zero(), f4zero()};
 #pragma unroll
     for (int i = 0; i < NIT; ++i) {
-      if (!live || !chunk_ok(i) || (a.dbg & 2)) continue;  // wave-uniform
+      if (!live || !chunk_ok(i)) continue;  // wave-uniform
       const int ci = i * ncw + cw, f0 = chunk_f0(i);
       const float* wsc = wsa + ci * 16 * g;
       const int whalf = nf * g;
@@ -446,7 +446,7 @@ __global__ __launch_bounds__(64 * RG_WAVES) void k_step_bwd_rg(const LayerK a) {
     }
     if (it == 0) RG_STAMP(stamp_base, 3);
     // ---- dX of the super tile: the chunk-waves' tiles summed in LDS, stored as the slice partial
-    if (dxw > 0 && !(a.dbg & 4)) {
+    if (dxw > 0) {
       float* redw = red + wave * TR * DP;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt)

@@ -123,9 +123,8 @@ __global__ __launch_bounds__(64 * NWV) void k_step_bwd_rw(const LayerK a) {
   const rsrc_t rws = make_rsrc(a.ws + (int64_t)chain * a.ws_cs, a.ws_cs);
   const rsrc_t rxd = make_rsrc(a.xrows + (int64_t)chain * a.xrow_cs, (int64_t)B * (d - a.gp));
   const rsrc_t ry = make_rsrc(a.yrows + (int64_t)chain * a.yrow_cs, (int64_t)B * a.y_cols);
-  // F_L complete (fused forward) / dX_{l+1} slice partials (a.dbg & 8: timing-only diagnostic
-  // reading one slice)
-  const int nsl = (a.last || (a.dbg & 8)) ? 1 : NSM;
+  // F_L complete (fused forward) / dX_{l+1} slice partials
+  const int nsl = a.last ? 1 : NSM;
   const int yc = a.likelihood == DGPRF_LIK_GAUSSIAN ? g : 1;
   float px[EX], pd[ED][NSM], py[ED];
   auto issue = [&](int rt) {

@@ -82,7 +82,7 @@ struct LayerK {
   // workgroup, ncw chunk-waves x nrw row-waves, register-prefetched prologue when rg_fast
   int32_t rt_per_rg, ncw, nrw, rg_fast, gred_off, rg_nit;
   int32_t rw_orows, rw_pad;  // row-wave backward: staged Omega rows (zero past d)
-  int32_t dbg;           // diagnostic switches (DGPRF_DBG env, never set in the product)
+  int32_t pad_d;
   int32_t cmp;           // row-group backward after the fused forward (step_fused_fwd): every
                          // F_l is complete in slice 0 of its partial buffer (one load, not 16)
   unsigned long long* stamps;  // -DDGPRF_STAMPS diagnostic build: stamp buffer, else null
@@ -537,7 +537,7 @@ inline LayerK make_layer_k(const dgprf_plan_t& pl, const StepDev& sd, int l, int
   a.pad_m = 0;
   a.rt_per_rg = 1;
   a.ncw = a.nrw = a.rg_fast = a.gred_off = a.rg_nit = 0;
-  a.dbg = a.cmp = 0;
+  a.pad_d = a.cmp = 0;
   a.rw_orows = a.rw_pad = 0;
   a.stamps = nullptr;
   return a;
@@ -618,6 +618,7 @@ inline bool rw_config(const dgprf_plan_t& pl, int l, bool fb, RwCfg& c, int max_
   c.orows = 4 * step_ks(d) > d ? 4 * step_ks(d) : d;
   const int xst = c.xst, dst = c.dst;
   if (!step_fused_fwd(pl) || pl.rt_per_group < 8 || d > 32 || g > 12 || dxw > 16 ||
+      pl.ws_chain >= (int64_t)1 << 29 ||
       (c.nch != 4 && c.nch != 8) || c.nch * (rbf ? 2 : 1) > 8 || pl.n_rf[l] % nf != 0)
     return false;
   // 16 waves (four per SIMD) when every wave still gets >= 2 row tiles and the layout fits

@@ -28,7 +28,6 @@
 // fragment loads are unconditional with clamped addresses (no exec-masked branches or per-load
 // waits) and are issued before the dependent partial sums; minibatch rows of step t+1 are gathered
 // by step t's update kernel, so the forward never waits on the step counter or the permutation.
-#include <cstdlib>
 #define DGPRF_STAMPS_TU
 
 #include "step_common.h"
@@ -462,20 +461,31 @@ __global__ __launch_bounds__(UPD_THREADS) void k_step_update(const UpdK a) {
 // random_fixed=False (layers/rf_layers.py:39-41): Omega_l = exp(lis_l)[:,None] z + mean_l[:,None]
 // with z ~ N(0,1) drawn for this step — Philox (seed, sub = step, DGPRF_RNG_Z, tag = 1 + l + 16
 // chain), element i of the layer at counter quad i / 4 — for the fresh layers.  One thread per
-// 4 elements; chain blockIdx.y writes its own workspace copy.
+// 4 elements; chain blockIdx.y writes its own workspace copy.  copy_fixed (the all-layer fused
+// forward reads every layer from this copy): the other layers' Omega is copied in from the
+// chain's Omega (chain stride om_cs), so the copy is the whole step's Omega.
 __global__ void k_fresh_omega(const dgprf_plan_t pl, const float* __restrict__ hyp, float* ws,
-                              const int64_t* step, uint64_t seed, int32_t step_offset) {
+                              const int64_t* step, uint64_t seed, int32_t step_offset,
+                              const float* __restrict__ omega, int64_t om_cs, int32_t copy_fixed) {
   const int chain = blockIdx.y;
   const int64_t i0 = 4 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
   if (i0 >= pl.omega_total) return;
   int layer = 0;
   for (int l = 1; l < pl.n_layers; ++l)
     if (i0 >= pl.omega_off[l]) layer = l;
-  if (!((pl.fresh_z >> layer) & 1)) return;
-  const float* h = hyp + (pl.hyp_per_chain ? (int64_t)chain * pl.hyp_total : 0);
   float* om = ws + (int64_t)chain * pl.ws_chain + pl.omf_off;
   const int64_t n_l = (int64_t)pl.d[layer] * pl.n_rf[layer];
   const int64_t j0 = i0 - pl.omega_off[layer];  // omega_off is a multiple of 4
+  if (!((pl.fresh_z >> layer) & 1)) {
+    if (copy_fixed) {
+      const float* src = omega + (int64_t)chain * om_cs;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (j0 + c < n_l) om[i0 + c] = src[i0 + c];
+    }
+    return;
+  }
+  const float* h = hyp + (pl.hyp_per_chain ? (int64_t)chain * pl.hyp_total : 0);
   const int64_t t = *step + step_offset;
   const f4 z = philox_normal4(seed, (uint64_t)t, DGPRF_RNG_Z, 1u + layer + 16u * chain,
                               (uint32_t)(j0 >> 2));
@@ -506,6 +516,7 @@ struct AgemmK {
   float* aout;         // [align32(B)][R] of chain 0 (stride ws_cs)
   int64_t xrow_cs, om_cs, ws_cs;
   int32_t B, d, R, d_in;
+  int32_t n_out, pad;  // rows of aout written (>= B; rows >= B are zeros)
 };
 constexpr int AG_KB = 32, AG_XST = 33, AG_OST = 68;
 
@@ -572,6 +583,7 @@ __global__ __launch_bounds__(256) void k_step_agemm(const AgemmK a) {
   for (int r = 0; r < 4; ++r) {
     const int64_t row = rb + wr * 16 + 4 * lq + r;
     const int f = fb + wc * 32 + lr;
+    if (row >= a.n_out) continue;
     if (f < R) out[row * R + f] = acc0[r];
     if (f + 16 < R) out[row * R + f + 16] = acc1[r];
   }
@@ -624,16 +636,6 @@ extern "C" int dgprf_debug_clear_stamps(void) {
 
 namespace dgprf {
 
-// Which A_1 GEMM runs: the hand-written MFMA kernel (agemm.hip) unless DGPRF_AGEMM=lib asks for
-// hipBLASLt (the comparison arm of scripts/diag/agemm_cmp.py); k_step_agemm for shapes outside both.
-static bool agemm_lib() {
-  static const int v = [] {
-    const char* e = getenv("DGPRF_AGEMM");
-    return e && e[0] == 'l' ? 1 : 0;
-  }();
-  return v != 0;
-}
-
 // A_1 = X Omega_1 of the step's gathered rows into the workspace (plan.a0_off).
 hipError_t launch_step_agemm(const dgprf_plan_t& pl, const StepDev& sd, hipStream_t s) {
   int lds_floats = 0;
@@ -641,13 +643,10 @@ hipError_t launch_step_agemm(const dgprf_plan_t& pl, const StepDev& sd, hipStrea
   if (!a.a0) return hipSuccess;
   hipError_t err = hipSuccess;
   const int64_t rows = (pl.batch + 31) / 32 * 32;  // the [align32(B)][R] buffer, zero-padded
-  if (!agemm_lib() && own_agemm(a.xrows, pl.batch, rows, pl.d_in, pl.d[0], a.om, pl.n_rf[0],
-                                sd.ws + pl.a0_off, pl.n_chains, a.xrow_cs, a.om_cs, pl.ws_chain, s,
-                                &err))
+  // the hand-written MFMA GEMM (agemm.hip); k_step_agemm for shapes outside it
+  if (own_agemm(a.xrows, pl.batch, rows, pl.d_in, pl.d[0], a.om, pl.n_rf[0], sd.ws + pl.a0_off,
+                pl.n_chains, a.xrow_cs, a.om_cs, pl.ws_chain, s, &err))
     return err;
-  if (agemm_lib() && blas_agemm(a.xrows, pl.batch, pl.d_in, pl.d[0], a.om, pl.n_rf[0],
-                                sd.ws + pl.a0_off, pl.n_chains, a.xrow_cs, a.om_cs, pl.ws_chain, s))
-    return hipSuccess;
   AgemmK g;
   g.xrows = a.xrows;
   g.om = a.om;
@@ -659,6 +658,8 @@ hipError_t launch_step_agemm(const dgprf_plan_t& pl, const StepDev& sd, hipStrea
   g.d = pl.d[0];
   g.R = pl.n_rf[0];
   g.d_in = pl.d_in;
+  g.n_out = (int32_t)rows;
+  g.pad = 0;
   dim3 ggrid((unsigned)((g.R + 63) / 64), (unsigned)((g.B + 31) / 32), pl.n_chains);
   hipLaunchKernelGGL(k_step_agemm, ggrid, dim3(256), 0, s, g);
   return hipGetLastError();
@@ -698,9 +699,9 @@ hipError_t launch_step_fwd_fused(const dgprf_plan_t& pl, const StepDev& sd, hipS
 
 hipError_t launch_step_bwd(const dgprf_plan_t& pl, const StepDev& sd, int layer, hipStream_t s) {
   RwCfg w;
-  static const bool no_rw = getenv("DGPRF_NO_RW") != nullptr;  // diagnostic: row-group kernel only
-  static const int rw_max = getenv("DGPRF_RW_NWV") ? atoi(getenv("DGPRF_RW_NWV")) : 16;  // diagnostic
-  if (pl.rt_per_group > 1 && !no_rw && rw_config(pl, layer, sd.full_bayes != 0, w, rw_max)) {
+  if (pl.rt_per_group > 1 && pl.ws_chain >= (int64_t)1 << 29)
+    return hipErrorInvalidValue;  // 32-bit buffer offsets of the row-group / row-wave kernels
+  if (pl.rt_per_group > 1 && rw_config(pl, layer, sd.full_bayes != 0, w)) {
     // row-wave backward (narrow slices after the fused forward): no barrier in the row-tile loop
     int lds_floats = 0;
     LayerK a = make_layer_k(pl, sd, layer, lds_floats, /*bwd=*/true, 4);
@@ -709,7 +710,6 @@ hipError_t launch_step_bwd(const dgprf_plan_t& pl, const StepDev& sd, int layer,
     a.main_blocks = 8 * a.rt_per_xcd * a.ns;
     a.rt_per_rg = pl.rt_per_group;
     a.cmp = 1;
-    if (const char* dbg = getenv("DGPRF_DBG_RW")) a.dbg = atoi(dbg);  // diagnostic only
     a.wsa_off = w.wsa;
     a.osa_off = w.osa;
     a.osa_st = w.ost;
@@ -754,7 +754,6 @@ hipError_t launch_step_bwd(const dgprf_plan_t& pl, const StepDev& sd, int layer,
     a.osa_st = c.ost;
     a.hred_off = c.hred;
     a.gred_off = c.gred;
-    if (const char* dbg = getenv("DGPRF_DBG_RG")) a.dbg = atoi(dbg);
     a.cmp = step_fused_fwd(pl) ? 1 : 0;
 #ifdef DGPRF_STAMPS
     a.stamps = rg_stamp_buffer();
@@ -899,10 +898,7 @@ hipError_t launch_agemm(const float* X, int64_t n, int ld, int d, const float* o
                         float* aout, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipError_t err = hipSuccess;
-  if (!agemm_lib() && n <= INT32_MAX && own_agemm(X, n, n, ld, d, om, R, aout, 1, 0, 0, 0, s, &err))
-    return err;
-  if (agemm_lib() && n <= INT32_MAX && blas_agemm(X, n, ld, d, om, R, aout, 1, 0, 0, 0, s))
-    return hipSuccess;
+  if (n <= INT32_MAX && own_agemm(X, n, n, ld, d, om, R, aout, 1, 0, 0, 0, s, &err)) return err;
   if (n > INT32_MAX || (int64_t)n * ld >= ((int64_t)1 << 29) || (int64_t)d * R >= ((int64_t)1 << 29))
     return hipErrorInvalidValue;  // 32-bit buffer offsets
   AgemmK g;
@@ -914,6 +910,8 @@ hipError_t launch_agemm(const float* X, int64_t n, int ld, int d, const float* o
   g.d = d;
   g.R = R;
   g.d_in = ld;
+  g.n_out = (int32_t)n;
+  g.pad = 0;
   dim3 grid((unsigned)((R + 63) / 64), (unsigned)((n + 31) / 32), 1);
   hipLaunchKernelGGL(k_step_agemm, grid, dim3(256), 0, s, g);
   return hipGetLastError();
@@ -942,7 +940,7 @@ hipError_t launch_fresh_omega(const dgprf_plan_t& pl, const StepDev& sd, hipStre
   const int64_t quads = (pl.omega_total + 3) / 4;
   dim3 grid((unsigned)((quads + 255) / 256), pl.n_chains);
   hipLaunchKernelGGL(k_fresh_omega, grid, dim3(256), 0, s, pl, sd.hyp, sd.ws, sd.step, sd.seed,
-                     sd.step_offset);
+                     sd.step_offset, sd.omega, sd.om_cs, step_fused_fwd(pl) ? 1 : 0);
   return hipGetLastError();
 }
 

@@ -22,7 +22,7 @@ RNG_NOISE, RNG_RESAMPLE, RNG_Z, RNG_W, RNG_MOMENTS = 1, 2, 3, 4, 5
 RNG_HYPER, RNG_HYPER_RESAMPLE = 6, 7
 HYP_KERNEL, HYP_LIK, HYP_MEAN = 1, 2, 4
 HMASS = 32  # hmass slots: log_amp l -> l, log_inv_ls l -> 8 + l, mean l -> 16 + l, lik_log_var -> 24
-ABI_VERSION = 6
+ABI_VERSION = 7
 FWD_AUTO, FWD_ROWS, FWD_NO_AGEMM, FWD_TILE, FWD_ROWS16, FWD_ROWS8 = 0, 1, 2, 3, 4, 5
 
 E_ARG, E_SHAPE, E_HIP, E_PLAN = -1, -2, -3, -4
@@ -42,7 +42,7 @@ class Plan(ctypes.Structure):
         ("likelihood", _i32), ("batch", _i32), ("n_chains", _i32),
         ("kind", _i32 * _L), ("n_rf", _i32 * _L), ("n_gp", _i32 * _L),
         ("hyp_flags", _i32), ("hyp_per_chain", _i32), ("ard", _i32 * _L),
-        ("fwd_path", _i32), ("agemm_chunk_rows", _i32), ("fresh_z", _i32),
+        ("fwd_path", _i32), ("agemm_chunk_rows", _i32), ("fresh_z", _i32), ("bwd_tiles", _i32),
         ("initialised", _i32),
         ("d", _i32 * _L), ("P", _i32 * _L), ("ns", _i32 * _L), ("cpw", _i32 * _L),
         ("n_row_tiles", _i32), ("n_rt_pad", _i32), ("rt_per_group", _i32), ("n_gw_rows", _i32),
@@ -106,6 +106,7 @@ SIGNATURES = {
     "dgprf_rf_omega": (_i32, [_i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "dgprf_rf_features": (_i32, [_i32, _vp, _i64, _i32, _vp, _i32, _vp, _vp, _vp]),
     "dgprf_gp_matmul": (_i32, [_vp, _i64, _i32, _vp, _i32, _vp, _vp]),
+    "dgprf_rf_project": (_i32, [_vp, _i64, _i32, _i32, _vp, _i32, _vp, _vp]),
     "dgprf_prior_w": (_i32, [ctypes.POINTER(Plan), _vp, _vp, _vp]),
     "dgprf_sghmc_update": (_i32, [ctypes.POINTER(Plan), _vp, _vp, _vp, _vp, _vp, _u64,
                                   ctypes.POINTER(Step), _vp]),

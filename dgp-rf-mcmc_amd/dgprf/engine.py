@@ -200,6 +200,12 @@ class Engine:
         normal(None, N.RNG_W, out=self.theta)
         for l in range(self.L):
             self.lis_view(l).fill_(-0.5 * math.log(self.layout.d[l]))  # kernels/RBF.py:16-17,40
+        self.invalidate_omega()
+
+    def invalidate_omega(self):
+        """Forget the last Omega build: a native write to z or hyp (through a raw pointer) does not
+        bump torch's version counters, which build_omega_if_stale reads."""
+        self._omega_built_key = None
 
     def init_moments(self, hyper=False):
         """param.M = 1, param.moments ~ N(0,1) (models/dgp.py:235-240); hyper=True also for the
@@ -222,16 +228,24 @@ class Engine:
         return self.hyp[c * pl.hyp_total:(c + 1) * pl.hyp_total]
 
     # ---------------------------------------------------------------- per-B plans
-    def plan_ws(self, B, fresh_z=0):
+    def plan_ws(self, B, fresh_z=0, full_bayes=False):
         """(plan, zero-filled workspace) for minibatch size B; fresh_z = bit mask of the layers
-        that draw fresh z every step on the device (random_fixed=False, graph steps)."""
-        key = (int(B), int(fresh_z))
+        that draw fresh z every step on the device (random_fixed=False, graph steps).
+        full_bayes: a plan whose backward fits full_bayesian=True steps — when B > 256 and some
+        layer does not fit the full-Bayes row-group layout (rg_full_bayes == 0), the per-row-tile
+        backward (plan.bwd_tiles), sized for one gW partial row per 16-row tile."""
+        if full_bayes:
+            pl, ws = self.plan_ws(B, fresh_z)
+            if pl.rt_per_group == 1 or pl.rg_full_bayes:
+                return pl, ws
+        key = (int(B), int(fresh_z), bool(full_bayes))
         if key not in self._ws:
             pl = self.spec.plan(key[0], self.C, self.per_chain_hyp)
             # fresh z layers; a forward path pinned by set_forward_path also pins the step's
             # all-layer forward (large minibatches)
-            if fresh_z or self.layout.fwd_path != N.FWD_AUTO:
+            if fresh_z or full_bayes or self.layout.fwd_path != N.FWD_AUTO:
                 pl.fresh_z = key[1]
+                pl.bwd_tiles = int(key[2])
                 pl.fwd_path = self.layout.fwd_path
                 pl.agemm_chunk_rows = self.layout.agemm_chunk_rows
                 N.call("dgprf_plan_init", ctypes.byref(pl))
@@ -358,10 +372,10 @@ class Engine:
             self._plan_tensors[id(pl)] = t
         return t[1]
 
-    def _op_batch(self, X, Y, batch_size, mode, idx, perm_seed):
+    def _op_batch(self, X, Y, batch_size, mode, idx, perm_seed, full_bayes=False):
         X, Y = self._prep_batch(X, Y)
         B = X.shape[0] if mode == N.BATCH_DIRECT else int(batch_size)
-        pl, ws = self.plan_ws(B)
+        pl, ws = self.plan_ws(B, full_bayes=full_bayes)
         if idx is not None:
             idx = torch.as_tensor(idx).to(device=self.dev, dtype=torch.int32).contiguous()
         iters = X.shape[0] // B if mode == N.BATCH_EPOCH else 0
@@ -375,7 +389,8 @@ class Engine:
         (models/dgp.py:199-216); Omega, c and sigma^2 are rebuilt on the device afterwards."""
         if full_bayes:
             self._check_full_bayes()
-        pl, ws, X, Y, idx, iters, ps = self._op_batch(X, Y, batch_size, mode, idx, perm_seed)
+        pl, ws, X, Y, idx, iters, ps = self._op_batch(X, Y, batch_size, mode, idx, perm_seed,
+                                                      full_bayes)
         if build:
             self.build_omega()
         dv = lambda t: None if t is None else as_device(t, self.dev)
@@ -392,7 +407,8 @@ class Engine:
         w.r.t. every trainable variable -> [C, w_total + hyp_total] (hyp layout after W)."""
         if full_bayes and self.C > 1 and not self.per_chain_hyp:
             raise ValueError("full_bayesian=True with several chains needs per_chain_hyp=True")
-        pl, ws, X, Y, idx, iters, ps = self._op_batch(X, Y, batch_size, mode, idx, perm_seed)
+        pl, ws, X, Y, idx, iters, ps = self._op_batch(X, Y, batch_size, mode, idx, perm_seed,
+                                                      full_bayes)
         if build:
             self.build_omega()
         return ops().potential_grad(
@@ -421,7 +437,7 @@ class Engine:
             torch.cuda.current_stream(self.dev).synchronize()
             while len(self._graphs) >= self.MAX_GRAPHS:
                 self._graphs.pop(next(iter(self._graphs)))
-        pl, ws = self.plan_ws(batch_size, fresh_z)
+        pl, ws = self.plan_ws(batch_size, fresh_z, full_bayes)
         iters = X_all.shape[0] // int(batch_size)
         ch = self.chain_struct(ws)
         bt = self.batch_struct(X_all, Y_all, N.BATCH_EPOCH, iters=iters, perm_seed=perm_seed)
@@ -508,6 +524,20 @@ class Engine:
         self.layout.agemm_chunk_rows = int(agemm_chunk_rows)
         N.call("dgprf_plan_init", ctypes.byref(self.layout))
         self._plan_tensors.pop(id(self.layout), None)
+
+    def rf_project(self, X, omega, out=None):
+        """A = X Omega of one RF layer (layers/rf_layers.py:42, 88) through dgprf_rf_project — the
+        hand-written MFMA GEMM of the wide first layer.  X [n, >= d] (row stride X.shape[1]),
+        omega [d, R] -> A [n, R]."""
+        X = as_device(X, self.dev)
+        omega = as_device(omega, self.dev)
+        n, ldx = X.shape
+        d, R = omega.shape
+        if out is None:
+            out = torch.empty(n, R, dtype=_F32, device=self.dev)
+        N.call("dgprf_rf_project", ptr(X), int(n), int(ldx), int(d), ptr(omega), int(R), ptr(out),
+               stream())
+        return out
 
     def prior_w(self):
         out = torch.empty(self.C, dtype=_F32, device=self.dev)

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define DGPRF_ABI_VERSION 6
+#define DGPRF_ABI_VERSION 7
 
 #define DGPRF_MAX_LAYERS 8
 #define DGPRF_MAX_G 64        /* max latent GPs per layer (n_gp[l]) */
@@ -126,6 +126,10 @@ typedef struct dgprf_plan {
                               layers/rf_layers.py:39-41): the step builds that layer's Omega from
                               Philox (seed, sub = step, DGPRF_RNG_Z, tag = 1 + l + 16 chain) into
                               the workspace (omf_off).  W-only steps (not full_bayes). */
+  int32_t bwd_tiles;       /* 1: keep the per-row-tile backward (one gW partial row per 16-row tile)
+                              whatever B.  For full_bayesian=True steps / gradients at B > 256 when
+                              some layer does not fit the full-Bayes row-group layout
+                              (rg_full_bayes == 0, e.g. BASELINE config 4's 784-wide layer); ABI 7 */
   /* ---- derived by dgprf_plan_init ---- */
   int32_t initialised;
   int32_t d[DGPRF_MAX_LAYERS];      /* layer input width */
@@ -330,6 +334,13 @@ int dgprf_rf_features(int32_t kind, const float *X, int64_t n, int32_t d, const 
 /* GPLayer.__call__ (layers/GP_weight_layers.py:11-15): F[n][g] = Phi[n][P] W[P][g]. */
 int dgprf_gp_matmul(const float *phi, int64_t n, int32_t P, const float *W, int32_t g, float *F,
                     void *stream);
+/* The RF projection of one layer, A = X Omega (RBFLayer / ARCLayer `tf.matmul(x, self.Omega)`,
+ * layers/rf_layers.py:42, 88): A[n][R] = X[n][0:d] Omega[d][R], X with row stride ldx >= d, as the
+ * hand-written fp32 MFMA GEMM the wide first layer of the step and of the predictive forward runs
+ * (32 x 128 tiles up to 1,024 rows, 128 x 128 beyond).  d, ldx and R multiples of 4 for the MFMA
+ * kernel (other shapes take the LDS-tiled 16x16x4 fallback).  ABI 7. */
+int dgprf_rf_project(const float *X, int64_t n, int32_t ldx, int32_t d, const float *omega,
+                     int32_t R, float *A, void *stream);
 
 /* sum log N(W;0,1) per chain (DGP_RF.prior_W, models/dgp.py:129-136) into out[C]. */
 int dgprf_prior_w(const dgprf_plan_t *plan, const float *theta, float *out, void *stream);

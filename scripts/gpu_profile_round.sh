@@ -3,7 +3,7 @@
 # HBM-traffic PMC passes (FETCH_SIZE / WRITE_SIZE in separate passes, no trace domains).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 R=$PWD
-TAG=${TAG:-r03}
+TAG=${TAG:-r04}
 O=$R/gpurun_out/prof_$TAG
 mkdir -p $O
 export TMPDIR=/tmp

@@ -266,3 +266,43 @@ def test_wide_first_layer_full_bayes_grad(dev):
         lis = h[pl.lis_off[l]:pl.lis_off[l] + pl.d[l]]
         assert group_err(lis, ref["log_inv_ls"][l]) < 5e-4, ("lis", l)
     assert group_err([h[0], h[1]], [ref["log_amp"][0], ref["log_amp"][1]]) < 5e-4
+
+
+@pytest.mark.parametrize("n,d,ldx,R", [(200, 784, 784, 4096), (1024, 784, 784, 4096),
+                                       (1025, 784, 784, 4096), (10_000, 784, 784, 4096),
+                                       (77, 30, 33, 500), (1500, 36, 40, 1000)])
+def test_rf_project_agemm_tiles(dev, n, d, ldx, R):
+    """A = X Omega (layers/rf_layers.py:42) through dgprf_rf_project, the hand-written MFMA GEMM of
+    the wide first layer, against a float64 matmul to 2e-5 of the output scale: config 4's first
+    layer (d 784, R 4096) at the step's 200 rows and at 1,024 rows (32 x 128 tiles), and past the
+    switch at 1,025 and 10,000 rows (128 x 128 tiles, the benchmarked predictive chunk); a strided
+    X (ldx > d) with d % 4 == 0 at 1,500 rows (128 x 128, ragged in every dimension); d = 30 (the
+    LDS-tiled fallback kernel, rows written up to n only)."""
+    from dgprf import engine as E
+    from dgprf.engine import ModelSpec
+    from dgprf import _native as N
+    rng = np.random.default_rng(n + d)
+    Xs = rng.uniform(-0.5, 0.5, (n, ldx)).astype(np.float32)
+    om = (rng.standard_normal((d, R)) / np.sqrt(d)).astype(np.float32)
+    eng = E.Engine(ModelSpec(4, 1, [N.RBF], [8], [1]))
+    guard = torch.full((n + 40, R), 7.0, device=dev)  # rows past n must stay untouched
+    A = eng.rf_project(torch.as_tensor(Xs, device=dev), torch.as_tensor(om, device=dev),
+                       out=guard[:n])
+    torch.cuda.synchronize()
+    ref = Xs[:, :d].astype(np.float64) @ om.astype(np.float64)
+    got = cpu(A)
+    assert np.max(np.abs(got - ref)) < 2e-5 * np.max(np.abs(ref)), (n, d, R)
+    assert torch.all(guard[n:] == 7.0)
+
+
+def test_config4_predictive_rows_agemm_128(dev):
+    """Config 4's full model (784-wide first layer, 4 x RBF n_rf 4096, softmax) scored on a ragged
+    2,049-row test set in one A_1 chunk: the predictive path past 1,024 rows, whose A_1 GEMM runs
+    the 128 x 128 tile instance (the benchmarked 10,000-row path's kernel); per-row log p against
+    the float64 oracle (models/classification_model.py:49-60)."""
+    c = CONFIGS[4]
+    m, p = _model(c, 34)
+    Xt, Yt = _data(c, 2049, 204)
+    lp = cpu(m._engine.forward(Xt, Yt, logp=True)["logp"][0])
+    ref = O.log_prob(p, O.forward(p, Xt), Yt)
+    assert np.max(np.abs(lp - ref)) < 2e-5 * max(1.0, np.max(np.abs(ref)))

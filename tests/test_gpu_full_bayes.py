@@ -423,3 +423,38 @@ def test_full_bayes_per_chain_hyper_parameters(dev):
     F = eng.forward(X, f_out=True)["F"][0]
     for c in range(C):
         assert rel_err(cpu(F[c]), O.forward(ps[c], X)) < 2e-5, c
+
+
+def test_full_bayes_config4_shape_large_batch(dev):
+    """full_bayesian=True at BASELINE config 4's model shape (784-wide first layer, 4 x RBF n_rf
+    4096, g [30,30,30,10], softmax) with B = 600: the W-only row-group layout fits, the full-Bayes
+    one does not (staged X + hyper sums > 160 KiB), so the engine takes the per-row-tile backward
+    plan (plan.bwd_tiles) instead of failing with E_SHAPE.  Every gradient against the
+    oracle (W: 2e-4 of the gradient scale, the K = 8,192 contractions of config 4)."""
+    spec_args = (784, 10, ["RBF"] * 4, [4096] * 4, [30, 30, 30, 10], False, "softmax")
+    ard = [1] * 4
+    rng = np.random.default_rng(404)
+    eng = engine_for(spec_args, ard, ("kernel",))
+    p = random_params(rng, spec_args, ard)
+    for l in range(4):
+        p.mean[l] = np.zeros_like(p.mean[l])  # mean not trainable here: keep the default 0
+    load_chain(eng, p, 0)
+    B, N_ = 600, 60_000
+    pw = eng.plan_ws(B)[0]
+    assert pw.rt_per_group > 1 and pw.rg_full_bayes == 0
+    pf = eng.plan_ws(B, full_bayes=True)[0]
+    assert pf.rt_per_group == 1 and pf.bwd_tiles == 1 and pf.n_gw_rows == (B + 15) // 16
+    X = rng.uniform(-0.5, 0.5, (B, 784))
+    Y = rng.integers(0, 10, (B, 1)).astype(float)
+    tr = O.Trainable(kernel=True, lik=False, mean=False, ard=[True] * 4)
+    G = eng.grad(X, Y, N_, full_bayes=True)
+    ref = O.grad_full(p, X, Y, N_, tr)
+    pl = eng.layout
+    Gw = unpack(eng, G[:, :pl.w_total])
+    Gh = hyper_of(eng, G[0, pl.w_total:])
+    for l in range(4):
+        assert rel_err(Gw[l], ref["W"][l]) < 2e-4, ("W", l)
+        assert group_err(Gh["log_inv_ls"][l], ref["log_inv_ls"][l]) < 5e-4, ("lis", l)
+    assert group_err([Gh["log_amp"][l] for l in range(4)], [ref["log_amp"][l] for l in range(4)]) < 5e-4
+    # the W part equals the W-only row-group gradient up to fp32 summation order
+    assert rel_err(cpu(G[:, :pl.w_total]), cpu(eng.grad(X, Y, N_))) < 1e-5

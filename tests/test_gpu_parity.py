@@ -411,6 +411,38 @@ def test_graph_fresh_z_random_fixed_false(dev):
     assert rel_err(cpu(ea.theta), cpu(eb.theta)) < 1e-5
 
 
+def test_graph_fresh_z_partial_fused_forward(dev):
+    """random_fixed=False on ONE layer (fresh_z = 0b010) at B = 2,048 with one chain: the step runs
+    the all-layer fused forward, which reads every layer's Omega from the workspace copy — the
+    fixed layers' Omega must be copied there.  3 graph steps equal 3 eager steps of a
+    random_fixed=True twin whose layer-1 z is set to the device draws before each step."""
+    from dgprf import _native as N
+    from dgprf import engine as E
+    spec = E.ModelSpec(3, 1, [N.RBF, N.ARC, N.RBF], [64, 48, 32], [4, 4, 1], False,
+                       N.LIK_GAUSSIAN)
+    ea = E.Engine(spec, 1, seed=777)
+    ea.draw_init()
+    E.normal(None, N.RNG_W, out=ea.theta)
+    E.normal(None, N.RNG_MOMENTS, out=ea.mom)
+    ea.build_omega()
+    eb = E.Engine(spec, 1, seed=ea.seed)
+    for t in ("z", "hyp", "theta", "mom", "step_ctr"):
+        getattr(eb, t).copy_(getattr(ea, t))
+    n, B, lr, beta, T, steps = 8192, 2048, 0.01, 0.9, 1.0, 3
+    X = torch.randn(n, 3, device=dev)
+    Y = torch.randn(n, 1, device=dev)
+    pl, _ = ea.plan_ws(B, 0b010)
+    # the all-layer fused forward of the step (step_common.h step_fused_fwd)
+    assert pl.rt_per_group >= 8 and pl.n_chains == 1 and pl.a0_off < 0 and pl.omf_off >= 0
+    ea.graph(X, Y, B, n, lr, beta, T, steps, perm_seed=5, fresh_z=0b010).launch()
+    for t in range(steps):
+        z = R.philox_normal(pl.d[1] * pl.n_rf[1], ea.seed, t, R.PURPOSE_Z, tag=1 + 1)
+        eb.z_view(1).copy_(torch.as_tensor(z.reshape(pl.d[1], pl.n_rf[1]), dtype=torch.float32))
+        eb.step(X, Y, n, lr, beta, T, batch_size=B, mode=N.BATCH_EPOCH, perm_seed=5)
+    assert int(ea.step_ctr) == steps == int(eb.step_ctr)
+    assert rel_err(cpu(ea.theta), cpu(eb.theta)) < 1e-5
+
+
 def test_graph_fresh_z_two_chains(dev):
     """random_fixed=False with C = 2 chains in one graph: chain c draws its own z from Philox
     (seed, sub = step, RNG_Z, tag = 1 + l + 16 c) into its own workspace copy of Omega (chain
