@@ -63,6 +63,12 @@ __device__ __forceinline__ f4 bload4(rsrc_t r, uint32_t byte_off) {
 __device__ __forceinline__ float bload1(rsrc_t r, uint32_t byte_off) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
 }
+// Write-through store (cache policy sc1): the line goes on to the memory side instead of staying
+// dirty in this XCD's L2, so the kernel boundary does not pay its write-back (MI355X_MICROARCH.md,
+// price table row 'boundary': + bytes / 6 TB/s behind dirty fp32 partials).
+__device__ __forceinline__ void bstore1_wt(float v, rsrc_t r, uint32_t byte_off) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, byte_off, 0, 16);
+}
 
 // ---------------------------------------------------------------- Philox4x32-10
 struct u32x4 {

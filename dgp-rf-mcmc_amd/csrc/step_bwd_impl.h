@@ -237,6 +237,15 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
   for (int r = 0; r < 4; ++r) dg4[r] = G1 ? dfs[(4 * lq + r) * dfst] : 0.f;
 
   float* gwp = a.gwp + (int64_t)chain * a.ws_cs + (int64_t)rt * a.w_cs;
+#ifndef DGPRF_GWP_WT
+#define DGPRF_GWP_WT 0
+#endif
+  // this row tile's gW partial row: plain stores, or write-through (DGPRF_GWP_WT)
+  const rsrc_t rgw = make_rsrc(gwp, a.w_cs);
+  auto gw_store = [&](int64_t i, float v) {
+    if (DGPRF_GWP_WT) bstore1_wt(v, rgw, (uint32_t)(i * 4));
+    else gwp[i] = v;
+  };
   f4 dxa[4] = {f4zero(), f4zero(), f4zero(), f4zero()};
   // full_bayesian=True: per-wave sums over this row tile and the wave's features of
   //   hw[k]     = sum_b X[b][k] (dA z^T)[b][k]   (-> log_inv_ls)
@@ -356,8 +365,8 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
       }
       const int f = f0 + lr;
       if (lq == 0 && f < R) {
-        gwp[f] = gc;
-        if (RBF) gwp[R + f] = gs;
+        gw_store(f, gc);
+        if (RBF) gw_store(R + f, gs);
       }
     } else {
 #pragma unroll
@@ -376,8 +385,8 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
           for (int r = 0; r < 4; ++r) {
             const int f = f0 + 4 * lq + r;
             if (f < R) {
-              gwp[(int64_t)f * g + o] = gc[r];
-              if (RBF) gwp[(int64_t)(R + f) * g + o] = gs[r];
+              gw_store((int64_t)f * g + o, gc[r]);
+              if (RBF) gw_store((int64_t)(R + f) * g + o, gs[r]);
             }
           }
         }

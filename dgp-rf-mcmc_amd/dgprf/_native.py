@@ -148,7 +148,8 @@ def lib():
     return h
 
 
-TORCH_LIB_PATH = os.path.join(_HERE, "libdgprf_torch.so")
+# next to the C-ABI library it links ($ORIGIN), so a DGPRF_LIB build directory carries its own pair
+TORCH_LIB_PATH = os.path.join(os.path.dirname(LIB_PATH), "libdgprf_torch.so")
 _ops = None
 
 
