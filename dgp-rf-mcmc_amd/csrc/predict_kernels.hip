@@ -531,9 +531,6 @@ constexpr int TW_ROWS = TWW * TR;  // rows per workgroup
 #ifndef DGPRF_TILE_G8MIX
 #define DGPRF_TILE_G8MIX 0  // 1: G8 RBF cos half on 16x16x4 tiles (measured slower: 241 vs 221 us)
 #endif
-#ifndef DGPRF_TILE_G8ROW
-#define DGPRF_TILE_G8ROW 1  // g == 8 W staging: one interleaved row per lane pair, 16-byte writes
-#endif
 #ifndef DGPRF_TILE_G8
 #define DGPRF_TILE_G8 1  // layers with 2 <= g <= 8: F contraction on 4x4x1 MFMA blocks (no padding)
 #endif
@@ -633,21 +630,6 @@ __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
 #pragma unroll
           for (int t = 0; t < 4; ++t) v[t] = fb + e0 + t < R ? v[t] : 0.f;
           *reinterpret_cast<f4*>(wsb + h * 64 + e0) = v;
-        } else if (G8 && DGPRF_TILE_G8ROW && g == 8) {
-          // one W row (8 floats) per lane pair (the float4 of columns 0-3 in the even lane, 4-7 in
-          // the odd one): swap half a float4 with the partner lane and store the interleaved row
-          // [c0 c4 c1 c5 | c2 c6 c3 c7] as one 16-byte write per lane (no per-element index math
-          // or exec-masked scalar writes)
-          const int q = i - h * 16 * g, row = q >> 1, odd = q & 1;
-          const f4 v = fb + row < R ? sw[j] : f4zero();
-          const float r0 = __shfl_xor(odd ? v[0] : v[2], 1);
-          const float r1 = __shfl_xor(odd ? v[1] : v[3], 1);
-          f4 o;
-          o[0] = odd ? r0 : v[0];
-          o[1] = odd ? v[2] : r0;
-          o[2] = odd ? r1 : v[1];
-          o[3] = odd ? v[3] : r1;
-          *reinterpret_cast<f4*>(wsb + (h * 64 + row) * WST + 4 * odd) = o;
         } else if (G8) {
 #pragma unroll
           for (int t = 0; t < 4; ++t) {

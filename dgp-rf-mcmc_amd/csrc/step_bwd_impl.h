@@ -238,9 +238,11 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
 
   float* gwp = a.gwp + (int64_t)chain * a.ws_cs + (int64_t)rt * a.w_cs;
 #ifndef DGPRF_GWP_WT
-#define DGPRF_GWP_WT 0
+#define DGPRF_GWP_WT 1
 #endif
-  // this row tile's gW partial row: plain stores, or write-through (DGPRF_GWP_WT)
+  // this row tile's gW partial row, stored write-through (sc1): 13 rows x w_total floats at B = 200
+  // that would otherwise sit dirty in the XCD L2s when the launch ends (configs 4 / 5: 12.8 /
+  // 13.6 MB per layer; measured config 5 103 -> 98 us/step, config 4 126 -> 124)
   const rsrc_t rgw = make_rsrc(gwp, a.w_cs);
   auto gw_store = [&](int64_t i, float v) {
     if (DGPRF_GWP_WT) bstore1_wt(v, rgw, (uint32_t)(i * 4));

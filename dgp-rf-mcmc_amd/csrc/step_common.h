@@ -131,6 +131,7 @@ struct UpdK {
   uint64_t seed;
   int64_t ws_cs;
   int32_t step_offset, upd_blocks;
+  int32_t e_end, pad_e;  // parameters [0, e_end) are updated (e_end < w_total: the first layers only)
   UpdateDev ud;
   const float* grad_in;
   float* grad_out;
@@ -442,6 +443,97 @@ __device__ __forceinline__ void step_schedule(const UpdateDev& ud, int64_t t, fl
   }
 }
 
+
+// One lane's four packed parameters e0..e0+3 (one counter quad of Philox normals, 16-byte loads;
+// layer offsets are multiples of 4, so a quad never straddles two layers): the row-tile gW partials
+// summed in a fixed order, the prior term W/N, and m <- b m - h N g + sqrt(2(1-b) T M) xi,
+// theta <- theta + h m / M (models/dgp.py:206-216).  Parameters past e_end (or a layer's end) are
+// not stored.  GIN: gradient supplied (grad_in); GONLY: write the gradient (grad_out) instead.
+// (A ride-along form — layer l + 1's W updated by extra workgroups of layer l's backward launch —
+// measured slower: config 4 123.7 vs 116.3 us/step, config 5 98.0 vs 96.5)
+template <bool GIN, bool GONLY, bool XI, bool CYC, class K>
+__device__ __forceinline__ void w_update_quad(const K& a, const int e0, const int chain) {
+  const uint32_t off = (uint32_t)e0 * 4u;
+  const int64_t cw = (int64_t)chain * a.w_total;
+  int layer = 0;
+#pragma unroll
+  for (int l = 1; l < DGPRF_MAX_LAYERS; ++l)
+    if (l < a.n_layers && e0 >= a.lo[l]) layer = l;
+  // the mass and the step counter (written by the previous graph's k_advance) are loaded together
+  // with the parameters and partials: placed after the partial sums, the compiler issued them
+  // only once those had been waited for — a second dependent memory round trip per step
+  // layer padding between align4 offsets stays untouched: live elements of the quad (a.hi is
+  // indexed per lane, so this too is a memory load: issued here, not after the sums)
+  const int nlive = min(max(min(a.hi[layer], a.e_end) - e0, 0), 4);
+  const float M = GONLY ? 1.f : a.mass[chain * a.n_layers + layer];
+  const int64_t t = GONLY ? 0 : *a.step + (int64_t)a.step_offset;
+  const rsrc_t rth = make_rsrc(a.theta + cw, a.w_total);
+  const f4 th = bload4(rth, off);
+  f4 m = f4zero(), gr;
+  if (!GONLY) m = bload4(make_rsrc(a.mom + cw, a.w_total), off);
+  if constexpr (GIN) {
+    gr = bload4(make_rsrc(a.grad_in + cw, a.w_total), off);
+  } else {
+    // sum the row-tile gW partials in a fixed order: groups of 16 independent loads
+    const rsrc_t rs = make_rsrc(a.gwp + (int64_t)chain * a.ws_cs, (int64_t)a.n_rt * a.w_total);
+    f4 sacc = f4zero();
+    for (int rt0 = 0; rt0 < a.n_rt_pad; rt0 += 16) {
+      f4 v[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v[j] = bload4(rs, (uint32_t)(((rt0 + j) * a.w_total + e0) * 4));
+#pragma unroll
+      for (int j = 0; j < 16; ++j) sacc += v[j];
+    }
+    gr = sacc;
+  }
+#ifndef DGPRF_UPD_WT
+#define DGPRF_UPD_WT 0
+#endif
+  // theta / momenta / gradient stores (DGPRF_UPD_WT: write-through, the 2 w_total floats of a
+  // large model not left dirty in the L2s at the boundary to the next step's forward)
+  auto store = [&](float* base, f4 v) {  // base: the chain's array (w_total floats)
+    float* p = base + e0;
+    if (DGPRF_UPD_WT) {
+      const rsrc_t r = make_rsrc(base, a.w_total);
+      if (nlive == 4) {
+        bstore4_wt(v, r, off);
+      } else {
+        for (int k = 0; k < nlive; ++k) bstore1_wt(v[k], r, off + 4 * k);
+      }
+    } else if (nlive == 4) {
+      *reinterpret_cast<f4*>(p) = v;
+    } else {
+      for (int k = 0; k < nlive; ++k) p[k] = v[k];
+    }
+  };
+  const UpdateDev& ud = a.ud;
+  const float N = ud.data_size;
+  // dU/dW = W/N (prior N(0,1), models/dgp.py:129-136,171) + Phi^T dF (likelihood)
+  if (!GIN) gr = th / N + gr;
+  if constexpr (GONLY) {
+    store(a.grad_out + (int64_t)chain * a.grad_cs, gr);
+    return;
+  } else {
+    float lr, T;
+    int resample;
+    step_schedule<CYC>(ud, t, &lr, &T, &resample);
+    const float h = sqrtf(lr / N);
+    const float beta = ud.beta;
+    const uint32_t quad = (uint32_t)(e0 >> 2);
+    if (resample) {  // models/dgp.py:209-210 (ignores M, Appendix A.1)
+      if (XI && ud.xi_resample)  // lanes past w_total (the last block's tail) read 0, no access
+        m = bload4(make_rsrc(ud.xi_resample + cw, a.w_total), off);
+      else
+        m = philox_normal4(a.seed, (uint64_t)t, DGPRF_RNG_RESAMPLE, (uint32_t)chain, quad);
+    }
+    f4 mn = beta * m - (h * N) * gr;
+    const f4 eps = (XI && ud.xi) ? bload4(make_rsrc(ud.xi + cw, a.w_total), off)
+                                 : philox_normal4(a.seed, (uint64_t)t, DGPRF_RNG_NOISE, (uint32_t)chain, quad);
+    mn = mn + sqrtf(2.0f * (1.0f - beta) * T * M) * eps;
+    store(a.mom + cw, mn);
+    store(a.theta + cw, th + (h * (1.0f / M)) * mn);
+  }
+}
 
 // Minimum waves per SIMD the register allocation must allow.  Single-chain steps run one workgroup
 // per CU either way; with C chains per launch (13 x 16 x C workgroups) residency sets throughput:

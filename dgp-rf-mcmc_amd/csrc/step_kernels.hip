@@ -382,75 +382,8 @@ __global__ __launch_bounds__(UPD_THREADS) void k_step_update(const UpdK a) {
                  a.yb + (int64_t)chain * a.ws_cs, chain, t + 1, b);
     return;
   }
-  // four packed parameters per lane (one counter quad of Philox normals, 16-byte loads); layer
-  // offsets are multiples of 4, so a quad never straddles two layers
-  const int e0 = 4 * (bx * UPD_THREADS + (int)threadIdx.x);
-  const uint32_t off = (uint32_t)e0 * 4u;
-  const int64_t cw = (int64_t)chain * a.w_total;
-  int layer = 0;
-#pragma unroll
-  for (int l = 1; l < DGPRF_MAX_LAYERS; ++l)
-    if (l < a.n_layers && e0 >= a.lo[l]) layer = l;
-  // the mass and the step counter (written by the previous graph's k_advance) are loaded together
-  // with the parameters and partials: placed after the partial sums, the compiler issued them
-  // only once those had been waited for — a second dependent memory round trip per step
-  // layer padding between align4 offsets stays untouched: live elements of the quad (a.hi is
-  // indexed per lane, so this too is a memory load: issued here, not after the sums)
-  const int nlive = min(max(a.hi[layer] - e0, 0), 4);
-  const float M = GONLY ? 1.f : a.mass[chain * a.n_layers + layer];
-  const int64_t t = GONLY ? 0 : *a.step + (int64_t)a.step_offset;
-  const rsrc_t rth = make_rsrc(a.theta + cw, a.w_total);
-  const f4 th = bload4(rth, off);
-  f4 m = f4zero(), gr;
-  if (!GONLY) m = bload4(make_rsrc(a.mom + cw, a.w_total), off);
-  if (GIN) {
-    gr = bload4(make_rsrc(a.grad_in + cw, a.w_total), off);
-  } else {
-    // sum the row-tile gW partials in a fixed order: groups of 16 independent loads
-    const rsrc_t rs = make_rsrc(a.gwp + (int64_t)chain * a.ws_cs, (int64_t)a.n_rt * a.w_total);
-    f4 sacc = f4zero();
-    for (int rt0 = 0; rt0 < a.n_rt_pad; rt0 += 16) {
-      f4 v[16];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) v[j] = bload4(rs, (uint32_t)(((rt0 + j) * a.w_total + e0) * 4));
-#pragma unroll
-      for (int j = 0; j < 16; ++j) sacc += v[j];
-    }
-    gr = sacc;
-  }
-  auto store = [&](float* p, f4 v) {
-    if (nlive == 4) {
-      st4(p, v);
-    } else {
-      for (int k = 0; k < nlive; ++k) p[k] = v[k];
-    }
-  };
-  const UpdateDev& ud = a.ud;
-  const float N = ud.data_size;
-  // dU/dW = W/N (prior N(0,1), models/dgp.py:129-136,171) + Phi^T dF (likelihood)
-  if (!GIN) gr = th / N + gr;
-  if (GONLY) {
-    store(a.grad_out + (int64_t)chain * a.grad_cs + e0, gr);
-    return;
-  }
-  float lr, T;
-  int resample;
-  step_schedule<CYC>(ud, t, &lr, &T, &resample);
-  const float h = sqrtf(lr / N);
-  const float beta = ud.beta;
-  const uint32_t quad = (uint32_t)(e0 >> 2);
-  if (resample) {  // models/dgp.py:209-210 (ignores M, Appendix A.1)
-    if (XI && ud.xi_resample)  // lanes past w_total (the last block's tail) read 0, no access
-      m = bload4(make_rsrc(ud.xi_resample + cw, a.w_total), off);
-    else
-      m = philox_normal4(a.seed, (uint64_t)t, DGPRF_RNG_RESAMPLE, (uint32_t)chain, quad);
-  }
-  f4 mn = beta * m - (h * N) * gr;
-  const f4 eps = (XI && ud.xi) ? bload4(make_rsrc(ud.xi + cw, a.w_total), off)
-                               : philox_normal4(a.seed, (uint64_t)t, DGPRF_RNG_NOISE, (uint32_t)chain, quad);
-  mn = mn + sqrtf(2.0f * (1.0f - beta) * T * M) * eps;
-  store(a.mom + cw + e0, mn);
-  store(a.theta + cw + e0, th + (h * (1.0f / M)) * mn);
+  // four packed parameters per lane
+  w_update_quad<GIN, GONLY, XI, CYC>(a, 4 * (bx * UPD_THREADS + (int)threadIdx.x), chain);
 #ifdef DGPRF_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
@@ -809,6 +742,8 @@ hipError_t launch_step_update(const dgprf_plan_t& pl, const StepDev& sd, const U
   a.grad_in = grad_in;
   a.grad_out = sd.grad_out;
   a.grad_cs = pl.w_total + (sd.full_bayes ? pl.hyp_total : 0);
+  a.e_end = a.hi[pl.n_layers - 1];
+  a.pad_e = 0;
   a.gather_next = gather_next && sd.bd.mode == DGPRF_BATCH_EPOCH ? 1 : 0;
   a.B = pl.batch;
   a.d_in = pl.d_in;
@@ -816,7 +751,7 @@ hipError_t launch_step_update(const dgprf_plan_t& pl, const StepDev& sd, const U
   a.bd = sd.bd;
   a.xb = sd.ws ? sd.ws + pl.xb_off : nullptr;
   a.yb = sd.ws ? sd.ws + pl.yb_off : nullptr;
-  const int64_t quads = pl.w_total / 4;
+  const int64_t quads = ((int64_t)a.e_end + 3) / 4;
   a.upd_blocks = (int)((quads + UPD_THREADS - 1) / UPD_THREADS);
   const bool gin = grad_in != nullptr, gonly = ud.grad_only != 0;
   const bool fb = sd.full_bayes && !gin;
