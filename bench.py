@@ -473,10 +473,16 @@ def main():
     upd_bytes = 4 * pl.w_total * (pl.n_row_tiles + 2 + 2 + 2)  # gW partials + theta/mom r/w
     dom = max(per_name, key=lambda k: per_name[k][0] * per_name[k][2])
     ms_dom, fl_dom, _ = per_name[dom]
-    # duration per launch: this run's hipEvent measurement (`achieved` / `frac`); the committed
-    # rocprofv3 kernel trace of the same command (profiles/r04/) beside it as the cross-check
+    # duration per launch (`achieved` / `frac`): the dominant kernel's share of this run's timed
+    # region, live — the hipEvent step time over the K timed steps, split over the step's kernels
+    # in proportion to their event-pair times (each pair holds its kernel and one dependent-launch
+    # boundary), per launch.  The in-kernel span (pair minus an empty pair) is reported beside it
+    # (live_in_kernel_us), and the committed rocprofv3 kernel trace of the same command (profiles/
+    # r04/) as the cross-check (rocprof_avg_launch_us)
     rp_us = rocprof_avg_us(dom)
-    use_us = ms_dom * 1e3
+    n_dom = per_name[dom][2]
+    dom_pairs = inflow[:Lk] if dom == "k_step_fwd" else inflow[Lk:2 * Lk]
+    use_us = step_ms_dev * 1e3 * sum(dom_pairs) / sum(inflow) / n_dom
     n_launch = 2 * len(d) + 1
     bnd_us = launch_boundary_us(dev)
     rel = os.path.relpath(PROFILES, ROOT)
@@ -488,9 +494,13 @@ def main():
             "traffic_source": f"{rel}/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE "
                               "passes of this bench; bytes per launch incl. Infinity-Cache hits)",
             "avg_launch_us": round(use_us, 3),
-            "duration_source": "live: hipEvent pair around the kernel on its launch stream minus an "
-                               "empty pair (dgprf_profile_step, --profile-reps real steps), "
-                               "averaged over the kernel's L launches per step: the in-kernel span",
+            "duration_source": "live: the kernel's share of the timed region's hipEvent step time "
+                               "(step_us_events), split over the step's 2L+1 kernels by their "
+                               "event-pair times (dgprf_profile_step, --profile-reps real steps on "
+                               "the launch stream), per launch: kernel + its launch boundary",
+            "live_in_kernel_us": round(ms_dom * 1e3, 3),
+            "live_in_kernel_method": "event pair around the kernel minus an empty pair: the span "
+                                     "inside the kernel, without its launch boundary",
             "flops_per_launch": int(fl_dom),
             "rocprof_avg_launch_us": rp_us,
             "rocprof_frac": (round(fl_dom / (rp_us * 1e-6) / FP32_MFMA_PEAK, 8) if rp_us else None),

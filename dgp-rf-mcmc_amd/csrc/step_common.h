@@ -82,7 +82,7 @@ struct LayerK {
   // workgroup, ncw chunk-waves x nrw row-waves, register-prefetched prologue when rg_fast
   int32_t rt_per_rg, ncw, nrw, rg_fast, gred_off, rg_nit;
   int32_t rw_orows, rw_pad;  // row-wave backward: staged Omega rows (zero past d)
-  int32_t pad_d;
+  int32_t rw_one;         // row-wave backward: the dF source is one complete slice (= last)
   int32_t cmp;           // row-group backward after the fused forward (step_fused_fwd): every
                          // F_l is complete in slice 0 of its partial buffer (one load, not 16)
   unsigned long long* stamps;  // -DDGPRF_STAMPS diagnostic build: stamp buffer, else null
@@ -629,7 +629,7 @@ inline LayerK make_layer_k(const dgprf_plan_t& pl, const StepDev& sd, int l, int
   a.pad_m = 0;
   a.rt_per_rg = 1;
   a.ncw = a.nrw = a.rg_fast = a.gred_off = a.rg_nit = 0;
-  a.pad_d = a.cmp = 0;
+  a.rw_one = a.cmp = 0;
   a.rw_orows = a.rw_pad = 0;
   a.stamps = nullptr;
   return a;

@@ -643,6 +643,7 @@ hipError_t launch_step_bwd(const dgprf_plan_t& pl, const StepDev& sd, int layer,
     a.main_blocks = 8 * a.rt_per_xcd * a.ns;
     a.rt_per_rg = pl.rt_per_group;
     a.cmp = 1;
+    a.rw_one = a.last;
     a.wsa_off = w.wsa;
     a.osa_off = w.osa;
     a.osa_st = w.ost;
