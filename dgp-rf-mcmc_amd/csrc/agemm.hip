@@ -15,10 +15,16 @@
 // zeros; rows [n, n_out) of the output are written as zeros (the step's A_1 buffer is
 // [align32(B)][R] and its consumers read whole 16-row tiles).
 //
-// Tiles: BM = 32, BN = 128 for the step (B = 200: 7 x 32 = 224 workgroups, one per CU); 128 x 128
-// for larger n (10k rows: 79 x 32 = 2,528 workgroups).  Blocks that share an Omega column block
-// are dealt round-robin over the XCDs (row tile fastest), so each XCD's L2 holds its column
-// blocks for all of its row tiles.
+// Tiles: the step (n_out <= 1024 rows, B = 200 -> 224) runs 64 x 64 tiles in two K parts
+// (blockIdx.y = chain * 2 + part, part p -> output slab p, summed by the consumers, k_step_fwd /
+// k_step_bwd layer 0, as slab 0 + slab 1): 4 x 64 x 2 = 512 workgroups, two per CU, so one
+// workgroup's barrier and load waits overlap the other's MFMAs (one 32 x 128 tile per CU, K whole,
+// ran 24.5 us; 64 x 64 in two parts 20.6 us — scripts/microbench/agemm_variants.hip).  The step
+// tiles are dealt XCD-contiguously (workgroup b runs on XCD b % 8: XCD x takes tiles
+// [x G / 8, (x + 1) G / 8), row tile fastest), so each XCD's L2 holds the Omega column blocks of all
+// of its row tiles; the next k-step's LDS operands are read ahead of this k-step's MFMAs
+// (sched_group_barrier).  Larger n (predictive chunks, ~10k rows): 128 x 128 tiles (64 x 64 per
+// wave), K whole, blockIdx order (79 x 32 = 2,528 workgroups).
 #include "dgprf_internal.h"
 
 namespace {
@@ -34,12 +40,26 @@ constexpr int AG_BK = 32;
 struct AgArgs {
   const float* X;   // [n][ldx] of batch 0 (batch stride sx)
   const float* om;  // [d][R] of batch 0 (batch stride so; 0 = shared)
-  float* out;       // [n_out][R] of batch 0 (batch stride sa)
-  int64_t sx, so, sa;
+  float* out;       // [n_out][R] of batch 0 (batch stride sa); K part p at + p * sp
+  int64_t sx, so, sa, sp;
   int32_t n, n_out, ldx, d, R, n_mt;
 };
 
-template <int BM, int BN, int WM, int WN>
+// Workgroup b of G: XCD-contiguous tile order (XCD = b % 8 under round-robin dispatch; a pure speed
+// choice — any placement gives the same result), row tile fastest within an XCD's range.
+__device__ __forceinline__ void ag_tile(int b, int G, int n_mt, bool xcd, int& mt, int& nt) {
+  int L = b;
+  if (xcd) {
+    const int x = b & 7, j = b >> 3, q = G >> 3, r = G & 7;
+    L = x < r ? x * (q + 1) + j : r * (q + 1) + (x - r) * q + j;
+  }
+  mt = L % n_mt;
+  nt = L / n_mt;
+}
+
+// SK: K parts (blockIdx.y = batch * SK + part); SCHED: the next k-step's LDS reads are issued ahead
+// of this k-step's MFMAs (two register sets); XCD: ag_tile's XCD-contiguous order.
+template <int BM, int BN, int WM, int WN, int SK, bool SCHED, bool XCD>
 __global__ __launch_bounds__(256) void k_agemm(const AgArgs a) {
   static_assert((BM / WM) * (BN / WN) == 4, "4 waves per workgroup");
   constexpr int MT = WM / 32, NT = WN / 32;            // accumulator tiles per wave
@@ -49,12 +69,14 @@ __global__ __launch_bounds__(256) void k_agemm(const AgArgs a) {
   static_assert(A4 >= 1 && B4 >= 1, "tile too small for 256 threads");
   __shared__ float As[2][AG_BK * AST];
   __shared__ __attribute__((aligned(16))) float Bs[2][AG_BK * BN];
-  const int mt = blockIdx.x % a.n_mt, ntile = blockIdx.x / a.n_mt;
+  int mt, ntile;
+  ag_tile(blockIdx.x, gridDim.x, a.n_mt, XCD, mt, ntile);
   const int m0 = mt * BM, n0 = ntile * BN;
-  const int64_t bz = blockIdx.y;
+  const int64_t bz = blockIdx.y / SK;
+  const int part = SK > 1 ? (int)(blockIdx.y % SK) : 0;
   const float* X = a.X + bz * a.sx;
   const float* om = a.om + bz * a.so;
-  float* out = a.out + bz * a.sa;
+  float* out = a.out + bz * a.sa + part * a.sp;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wr = wave / (BN / WN), wc = wave % (BN / WN);
   const int n = a.n, d = a.d, R = a.R, ldx = a.ldx;
@@ -100,27 +122,55 @@ __global__ __launch_bounds__(256) void k_agemm(const AgArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  const int nkb = (d + AG_BK - 1) / AG_BK;
-  load(0);
+  // K part `part`: k-blocks [kb0, kb0 + nkb) (a part past d stages zeros and writes zeros)
+  const int nkb_all = (d + AG_BK - 1) / AG_BK, per = (nkb_all + SK - 1) / SK;
+  const int kb0 = part * per, nkb = max(0, min(per, nkb_all - kb0));
+  load(kb0 * AG_BK);
   store(0);
   __syncthreads();
   const int li = lane & 31, lk = lane >> 5;  // A[i][k] / B[k][j] operand lane map of 32x32x2
   for (int kb = 0; kb < nkb; ++kb) {
     const int buf = kb & 1;
-    if (kb + 1 < nkb) load((kb + 1) * AG_BK);
+    if (kb + 1 < nkb) load((kb0 + kb + 1) * AG_BK);
     const float* ap = &As[buf][lk * AST + wr * WM + li];
     const float* bp = &Bs[buf][lk * BN + wc * WN + li];
+    if (SCHED) {
+      float av[2][MT], bv[2][NT];
 #pragma unroll
-    for (int ks = 0; ks < AG_BK / 2; ++ks) {
-      float av[MT], bv[NT];
+      for (int i = 0; i < MT; ++i) av[0][i] = ap[32 * i];
 #pragma unroll
-      for (int i = 0; i < MT; ++i) av[i] = ap[2 * ks * AST + 32 * i];
+      for (int j = 0; j < NT; ++j) bv[0][j] = bp[32 * j];
 #pragma unroll
-      for (int j = 0; j < NT; ++j) bv[j] = bp[2 * ks * BN + 32 * j];
+      for (int ks = 0; ks < AG_BK / 2; ++ks) {
+        const int c = ks & 1;
+        if (ks + 1 < AG_BK / 2) {
 #pragma unroll
-      for (int i = 0; i < MT; ++i)
+          for (int i = 0; i < MT; ++i) av[c ^ 1][i] = ap[2 * (ks + 1) * AST + 32 * i];
 #pragma unroll
-        for (int j = 0; j < NT; ++j) acc[i][j] = mfma32(av[i], bv[j], acc[i][j]);
+          for (int j = 0; j < NT; ++j) bv[c ^ 1][j] = bp[2 * (ks + 1) * BN + 32 * j];
+        }
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+          for (int j = 0; j < NT; ++j) acc[i][j] = mfma32(av[c][i], bv[c][j], acc[i][j]);
+        // the scheduler otherwise sinks the reads below the MFMAs (one register set, every k-step
+        // waiting on its own reads): reads of ks + 1 first, then the MFMAs of ks
+        if (ks + 1 < AG_BK / 2) __builtin_amdgcn_sched_group_barrier(0x100, MT + NT, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, MT * NT, 0);
+      }
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < AG_BK / 2; ++ks) {
+        float av[MT], bv[NT];
+#pragma unroll
+        for (int i = 0; i < MT; ++i) av[i] = ap[2 * ks * AST + 32 * i];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) bv[j] = bp[2 * ks * BN + 32 * j];
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+          for (int j = 0; j < NT; ++j) acc[i][j] = mfma32(av[i], bv[j], acc[i][j]);
+      }
     }
     if (kb + 1 < nkb) store(buf ^ 1);
     __syncthreads();
@@ -139,12 +189,12 @@ __global__ __launch_bounds__(256) void k_agemm(const AgArgs a) {
     }
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int SK, bool SCHED, bool XCD>
 hipError_t agemm_launch(AgArgs a, int batch, hipStream_t s) {
   a.n_mt = (a.n_out + BM - 1) / BM;
   const int n_nt = (a.R + BN - 1) / BN;
-  dim3 grid((unsigned)(a.n_mt * n_nt), (unsigned)batch);
-  hipLaunchKernelGGL((k_agemm<BM, BN, WM, WN>), grid, dim3(256), 0, s, a);
+  dim3 grid((unsigned)(a.n_mt * n_nt), (unsigned)(batch * SK));
+  hipLaunchKernelGGL((k_agemm<BM, BN, WM, WN, SK, SCHED, XCD>), grid, dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
@@ -152,14 +202,26 @@ hipError_t agemm_launch(AgArgs a, int batch, hipStream_t s) {
 
 namespace dgprf {
 
-// false: the shape is outside this kernel (the caller falls back to k_step_agemm).
+bool agemm_shape_ok(int64_t n, int64_t n_out, int ldx, int d, int R) {
+  return n >= 1 && n_out >= n && d % 4 == 0 && ldx % 4 == 0 && R % 4 == 0 &&
+         n_out * (int64_t)R < ((int64_t)1 << 31) && n * (int64_t)ldx < ((int64_t)1 << 29) &&
+         (int64_t)d * R < ((int64_t)1 << 29);
+}
+
+int agemm_parts(int64_t n, int64_t n_out, int ldx, int d, int R) {
+  return agemm_shape_ok(n, n_out, ldx, d, R) && n_out <= 1024 ? 2 : 1;
+}
+
+// false: the shape is outside this kernel (the caller falls back to k_step_agemm).  parts = 2
+// (only as agemm_parts returns it): two K-part slabs sp floats apart, for consumers that sum them.
 bool own_agemm(const float* X, int64_t n, int64_t n_out, int ldx, int d, const float* om, int R,
-               float* aout, int batch, int64_t sx, int64_t so, int64_t sa, hipStream_t s,
-               hipError_t* err) {
-  if (n < 1 || n_out < n || d % 4 != 0 || ldx % 4 != 0 || R % 4 != 0 ||
-      n_out * (int64_t)R >= ((int64_t)1 << 31) || n * (int64_t)ldx >= ((int64_t)1 << 29) ||
-      (int64_t)d * R >= ((int64_t)1 << 29))
-    return false;
+               float* aout, int batch, int64_t sx, int64_t so, int64_t sa, int parts, int64_t sp,
+               hipStream_t s, hipError_t* err) {
+  if (!agemm_shape_ok(n, n_out, ldx, d, R)) return false;
+  if (parts != 1 && parts != agemm_parts(n, n_out, ldx, d, R)) {
+    *err = hipErrorInvalidValue;
+    return true;
+  }
   AgArgs a;
   a.X = X;
   a.om = om;
@@ -167,15 +229,17 @@ bool own_agemm(const float* X, int64_t n, int64_t n_out, int ldx, int d, const f
   a.sx = sx;
   a.so = so;
   a.sa = sa;
+  a.sp = sp;
   a.n = (int32_t)n;
   a.n_out = (int32_t)n_out;
   a.ldx = ldx;
   a.d = d;
   a.R = R;
   a.n_mt = 0;
-  // step-sized row counts: 32-row tiles so the grid covers the CUs; otherwise 128 x 128
-  *err = n_out <= 1024 ? agemm_launch<32, 128, 32, 32>(a, batch, s)
-                       : agemm_launch<128, 128, 64, 64>(a, batch, s);
+  // step-sized row counts: 64 x 64 tiles (K whole, or two parts); otherwise 128 x 128
+  if (parts == 2) *err = agemm_launch<64, 64, 32, 32, 2, true, true>(a, batch, s);
+  else if (n_out <= 1024) *err = agemm_launch<64, 64, 32, 32, 1, true, true>(a, batch, s);
+  else *err = agemm_launch<128, 128, 64, 64, 1, false, false>(a, batch, s);
   return true;
 }
 

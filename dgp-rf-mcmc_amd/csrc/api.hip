@@ -277,12 +277,12 @@ int dgprf_plan_init(dgprf_plan_t* pl) {
     pl->omf_off = ws;
     ws = align4(ws + om);
   }
-  // wide first layer: A_1 = X Omega_1 is one tiled GEMM per step (32-row tiles) instead of a
-  // d-long dependent k-step loop inside every forward / backward chunk
+  // wide first layer: A_1 = X Omega_1 is one tiled GEMM per step instead of a d-long dependent
+  // k-step loop inside every forward / backward chunk; two [align32(B)][R] slabs (its K parts)
   pl->a0_off = -1;
   if (pl->d[0] > 32) {
     pl->a0_off = ws;
-    ws = align4(ws + (int64_t)((B + 31) / 32 * 32) * pl->n_rf[0]);
+    ws = align4(ws + 2 * (int64_t)((B + 31) / 32 * 32) * pl->n_rf[0]);
   }
   pl->ws_chain = ws;
   pl->ws_total = ws * pl->n_chains;

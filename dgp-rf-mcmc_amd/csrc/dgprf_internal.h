@@ -110,11 +110,16 @@ hipError_t launch_advance(int64_t* step, int64_t by, hipStream_t s);
 // The step's A_1 GEMM alone (plan.a0_off >= 0): the hand-written MFMA kernel of agemm.hip.
 hipError_t launch_step_agemm(const dgprf_plan_t& pl, const StepDev& sd, hipStream_t s);
 // The hand-written MFMA A_1 GEMM (agemm.hip): A[n_out][R] = X[n][d] Omega[d][R] (rows >= n
-// zero) for `batch` chains (element strides sx, so, sa; so = 0: shared Omega).  false: shape
-// outside the kernel (d, ldx, R not multiples of 4, or too large for 32-bit offsets).
+// zero) for `batch` chains (element strides sx, so, sa; so = 0: shared Omega).  parts = 2: two
+// K-part slabs sp floats apart whose sum is A (the step's layer-0 consumers add them); parts = 1:
+// A whole.  false: shape outside the kernel (d, ldx, R not multiples of 4, or too large for
+// 32-bit offsets).
 bool own_agemm(const float* X, int64_t n, int64_t n_out, int ldx, int d, const float* om, int R,
-               float* aout, int batch, int64_t sx, int64_t so, int64_t sa, hipStream_t s,
-               hipError_t* err);
+               float* aout, int batch, int64_t sx, int64_t so, int64_t sa, int parts, int64_t sp,
+               hipStream_t s, hipError_t* err);
+bool agemm_shape_ok(int64_t n, int64_t n_out, int ldx, int d, int R);
+// K parts the step's A_1 GEMM writes (2 for step-sized row counts the kernel takes, else 1)
+int agemm_parts(int64_t n, int64_t n_out, int ldx, int d, int R);
 // plan.fresh_z: Omega of every layer into the workspace (omf_off), fresh layers from Philox z of
 // step *step + step_offset, the others copied from the chain's Omega when the all-layer fused
 // forward reads this copy (per-layer kernels read a fixed layer's Omega in place)

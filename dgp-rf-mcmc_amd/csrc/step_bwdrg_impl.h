@@ -337,13 +337,13 @@ __global__ __launch_bounds__(64 * RG_WAVES) void k_step_bwd_rg(const LayerK a) {
       f4 at_t;
       if (KS == 0 && a0) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) at_t[r] = a0[(int64_t)(4 * lq + r) * R + lr];
+        for (int r = 0; r < 4; ++r) at_t[r] = a0_sum1(a0 + (int64_t)(4 * lq + r) * R + lr, a.a0_sl);
       } else {
         at_t = a_tile<KS, true>(om, R, d, f0, omk[i], xf, xw, a.xst, lr, lq);
       }
       f4 at_n = f4zero(), dpc = f4zero(), dps = f4zero();
       if (dphi) {
-        at_n = (KS == 0 && a0) ? *reinterpret_cast<const f4*>(a0 + (int64_t)lr * R + 4 * lq)
+        at_n = (KS == 0 && a0) ? a0_sum4(a0 + (int64_t)lr * R + 4 * lq, a.a0_sl)
                                : a_tile<KS, false>(om, R, d, f0, omk[i], xf, xw, a.xst, lr, lq);
         if (G1) {
 #pragma unroll

@@ -77,7 +77,7 @@ struct LayerK {
   // block per chunk with a load round trip and two barriers each
   int32_t wstage, wsa_off, osa_off, osa_st, kind_rbf, pad_w;
   int32_t main_blocks;  // this layer's (row tile, slice) workgroups
-  int32_t pad_m;
+  int32_t a0_sl;  // layer 0 with a0: second K-part slab of A_1 at a0 + a0_sl (0: one slab)
   // row-group backward (k_step_bwd_rg, minibatches of > 16 row tiles): rt_per_rg row tiles per
   // workgroup, ncw chunk-waves x nrw row-waves, register-prefetched prologue when rg_fast
   int32_t rt_per_rg, ncw, nrw, rg_fast, gred_off, rg_nit;
@@ -87,6 +87,15 @@ struct LayerK {
                          // F_l is complete in slice 0 of its partial buffer (one load, not 16)
   unsigned long long* stamps;  // -DDGPRF_STAMPS diagnostic build: stamp buffer, else null
 };
+
+// A_1 elements at p: slab 0 + slab 1 of the GEMM's two K parts (sl = 0: one slab).  Every layer-0
+// consumer adds them in this order, so the forward and the backward see the same A_1.
+__device__ __forceinline__ f4 a0_sum4(const float* p, int sl) {
+  f4 v = *reinterpret_cast<const f4*>(p);
+  if (sl) v += *reinterpret_cast<const f4*>(p + sl);
+  return v;
+}
+__device__ __forceinline__ float a0_sum1(const float* p, int sl) { return sl ? p[0] + p[sl] : p[0]; }
 
 // Block -> (row tile, slice): blocks are dealt round-robin over the 8 XCDs, so block b's XCD group
 // is b % 8; every workgroup of row tile rt gets group rt % 8, so the slice partials it exchanges
@@ -626,7 +635,12 @@ inline LayerK make_layer_k(const dgprf_plan_t& pl, const StepDev& sd, int l, int
   a.hred_off = lds_floats;
   if (sd.full_bayes) lds_floats += NW * round4(2 * a.d + 1);
   a.main_blocks = 8 * a.rt_per_xcd * a.ns;
-  a.pad_m = 0;
+  a.a0_sl = 0;
+  if (a.a0) {  // the A_1 GEMM's K parts (agemm.hip): two slabs, summed here as slab 0 + slab 1
+    const int64_t rows = (pl.batch + 31) / 32 * 32;
+    if (dgprf::agemm_parts(pl.batch, rows, pl.d_in, pl.d[0], pl.n_rf[0]) == 2)
+      a.a0_sl = (int32_t)(rows * pl.n_rf[0]);
+  }
   a.rt_per_rg = 1;
   a.ncw = a.nrw = a.rg_fast = a.gred_off = a.rg_nit = 0;
   a.rw_one = a.cmp = 0;

@@ -52,7 +52,7 @@ __global__ __launch_bounds__(64 * NWB) void k_step_fwd(const LayerK a) {
   for (int i = 0; i < nit; ++i) {
     const int f0 = chunk_f0(i);
     if (f0 >= R) break;
-    const f4 at = (KS == 0 && a0) ? *reinterpret_cast<const f4*>(a0 + f0 + 4 * lq)
+    const f4 at = (KS == 0 && a0) ? a0_sum4(a0 + f0 + 4 * lq, a.a0_sl)
                                   : a_tile<KS, false>(om, R, d, f0, omk, xf, xs, a.xst, lr, lq);
     float p0[4], p1[4];
     features<RBF>(at, cl, p0, p1);

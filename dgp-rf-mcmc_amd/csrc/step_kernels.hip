@@ -578,7 +578,7 @@ hipError_t launch_step_agemm(const dgprf_plan_t& pl, const StepDev& sd, hipStrea
   const int64_t rows = (pl.batch + 31) / 32 * 32;  // the [align32(B)][R] buffer, zero-padded
   // the hand-written MFMA GEMM (agemm.hip); k_step_agemm for shapes outside it
   if (own_agemm(a.xrows, pl.batch, rows, pl.d_in, pl.d[0], a.om, pl.n_rf[0], sd.ws + pl.a0_off,
-                pl.n_chains, a.xrow_cs, a.om_cs, pl.ws_chain, s, &err))
+                pl.n_chains, a.xrow_cs, a.om_cs, pl.ws_chain, a.a0_sl ? 2 : 1, a.a0_sl, s, &err))
     return err;
   AgemmK g;
   g.xrows = a.xrows;
@@ -834,7 +834,7 @@ hipError_t launch_agemm(const float* X, int64_t n, int ld, int d, const float* o
                         float* aout, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipError_t err = hipSuccess;
-  if (n <= INT32_MAX && own_agemm(X, n, n, ld, d, om, R, aout, 1, 0, 0, 0, s, &err)) return err;
+  if (n <= INT32_MAX && own_agemm(X, n, n, ld, d, om, R, aout, 1, 0, 0, 0, 1, 0, s, &err)) return err;
   if (n > INT32_MAX || (int64_t)n * ld >= ((int64_t)1 << 29) || (int64_t)d * R >= ((int64_t)1 << 29))
     return hipErrorInvalidValue;  // 32-bit buffer offsets
   AgemmK g;

@@ -274,8 +274,10 @@ def test_wide_first_layer_full_bayes_grad(dev):
 def test_rf_project_agemm_tiles(dev, n, d, ldx, R):
     """A = X Omega (layers/rf_layers.py:42) through dgprf_rf_project, the hand-written MFMA GEMM of
     the wide first layer, against a float64 matmul to 2e-5 of the output scale: config 4's first
-    layer (d 784, R 4096) at the step's 200 rows and at 1,024 rows (32 x 128 tiles), and past the
-    switch at 1,025 and 10,000 rows (128 x 128 tiles, the benchmarked predictive chunk); a strided
+    layer (d 784, R 4096) at the step's 200 rows and at 1,024 rows (64 x 64 tiles, K whole: the
+    step itself runs them in two K parts, summed by its layer-0 kernels and covered by the config-4
+    step parity tests), and past the switch at 1,025 and 10,000 rows (128 x 128 tiles, the
+    benchmarked predictive chunk); a strided
     X (ldx > d) with d % 4 == 0 at 1,500 rows (128 x 128, ragged in every dimension); d = 30 (the
     LDS-tiled fallback kernel, rows written up to n only)."""
     from dgprf import engine as E
