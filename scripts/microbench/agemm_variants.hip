@@ -56,7 +56,7 @@ __device__ __forceinline__ void tile_of(const Args& a, int b, int G, int& mt, in
 
 // ---------------------------------------------------------------- V1: the shipped kernel shape
 // 32x32x2, X staged transposed [BK][BM+1], Omega [BK][BN], register-staged double buffer.
-template <int BM, int BN, int WM, int WN, int PF>
+template <int BM, int BN, int WM, int WN, int PF, int EPI = 0>
 __global__ __launch_bounds__(256) void k_v1(const Args a) {
   constexpr int BK = 32;
   constexpr int MT = WM / 32, NT = WN / 32;
@@ -174,6 +174,28 @@ __global__ __launch_bounds__(256) void k_v1(const Args a) {
     }
     if (kb + 1 < nkb) store(buf ^ 1);
     __syncthreads();
+  }
+  if (EPI) {  // accumulators -> LDS (per wave [WM][WN + 4]) -> 16-byte row stores
+    constexpr int EST = WN;  // (the two lane halves of a ds_write_b32 are separate bank groups)
+    static_assert(4 * WM * EST <= 2 * BK * (AST + BN), "epilogue staging");
+    float* eb = &As[0][0] + wave * WM * EST;  // As and Bs are contiguous
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          eb[(32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk) * EST + 32 * j + li] = acc[i][j][r];
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): own wave's writes (wave-private region)
+#pragma unroll
+    for (int e = lane; e < WM * WN / 4; e += 64) {
+      const int rr = e / (WN / 4), c4 = e % (WN / 4);
+      const int row = m0 + wr * WM + rr, col = n0 + wc * WN + 4 * c4;
+      const f4 v = *reinterpret_cast<const f4*>(eb + rr * EST + 4 * c4);
+      if (row < a.n_out && col < a.R)
+        *reinterpret_cast<f4*>(out + (int64_t)row * a.R + col) = row < a.n ? v : f4{0.f, 0.f, 0.f, 0.f};
+    }
+    return;
   }
 #pragma unroll
   for (int i = 0; i < MT; ++i)
@@ -443,16 +465,16 @@ float run_v3(Args a, int reps) {
   return ms * 1e3f / reps;
 }
 
-template <int BM, int BN, int WM, int WN, int PF>
+template <int BM, int BN, int WM, int WN, int PF, int EPI = 0>
 float run_v1(Args a, int reps) {
   a.n_mt = (a.n_out + BM - 1) / BM;
   dim3 grid(a.n_mt * ((a.R + BN - 1) / BN), a.ksplit);
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  hipLaunchKernelGGL((k_v1<BM, BN, WM, WN, PF>), grid, dim3(256), 0, 0, a);
+  hipLaunchKernelGGL((k_v1<BM, BN, WM, WN, PF, EPI>), grid, dim3(256), 0, 0, a);
   CK(hipEventRecord(e0));
-  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL((k_v1<BM, BN, WM, WN, PF>), grid, dim3(256), 0, 0, a);
+  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL((k_v1<BM, BN, WM, WN, PF, EPI>), grid, dim3(256), 0, 0, a);
   CK(hipEventRecord(e1));
   CK(hipEventSynchronize(e1));
   float ms;
@@ -1077,34 +1099,19 @@ int main() {
       fflush(stdout);
     };
     if (s.n_out <= 1024) {
-      rep("v1 32x128 w32x32 pf0", run_v1<32, 128, 32, 32, 0>(a, s.reps));
       a.gm = 1000;
-      rep("v1 64x64 w32x32 pf3 xcd", run_v1<64, 64, 32, 32, 3>(a, s.reps));
       a.ksplit = 2;
       rep("v1 64x64 w32x32 pf3 xcd sk2", run_v1<64, 64, 32, 32, 3>(a, s.reps), 2);
-      rep("v1 32x128 w32x32 pf3 xcd sk2", run_v1<32, 128, 32, 32, 3>(a, s.reps), 2);
-      rep("v1 64x128 w32x64 pf3 xcd sk2", run_v1<64, 128, 32, 64, 3>(a, s.reps), 2);
-      a.ksplit = 4;
-      rep("v1 64x64 w32x32 pf3 xcd sk4", run_v1<64, 64, 32, 32, 3>(a, s.reps), 4);
-      rep("v1 64x128 w32x64 pf3 xcd sk4", run_v1<64, 128, 32, 64, 3>(a, s.reps), 4);
-      rep("v1 128x128 w64x64 pf3 xcd sk4", run_v1<128, 128, 64, 64, 3>(a, s.reps), 4);
+      rep("v1 64x64 w32x32 pf3 xcd sk2 epi", run_v1<64, 64, 32, 32, 3, 1>(a, s.reps), 2);
       a.ksplit = 1;
       a.gm = 0;
-      rep("v5 32x128 split-K 2", run_v5<32, 128, 32, 32, 2>(a, s.reps), 2);
-      rep("v1 32x128 w32x32 pf0 (again)", run_v1<32, 128, 32, 32, 0>(a, s.reps));
     } else {
       rep("v1 128x128 w64x64 pf0", run_v1<128, 128, 64, 64, 0>(a, s.reps));
-      rep("v1 128x128 w64x64 pf1", run_v1<128, 128, 64, 64, 1>(a, s.reps));
-      rep("v1 128x128 w64x64 pf2", run_v1<128, 128, 64, 64, 2>(a, s.reps));
-      rep("v1 128x128 w64x64 pf3", run_v1<128, 128, 64, 64, 3>(a, s.reps));
-      rep("v8 128x128 w64x64 ks1 bk32", run_v8<128, 128, 64, 64, 1, 32>(a, s.reps));
-      rep("v8 256x128 w64x64 ks1 bk32", run_v8<256, 128, 64, 64, 1, 32>(a, s.reps));
-      rep("v8 128x256 w64x64 ks1 bk32", run_v8<128, 256, 64, 64, 1, 32>(a, s.reps));
-      rep("v8 128x256 w64x128 ks1 bk32", run_v8<128, 256, 64, 128, 1, 32>(a, s.reps));
-      rep("v8 256x128 w128x64 ks1 bk32", run_v8<256, 128, 128, 64, 1, 32>(a, s.reps));
-      rep("v8 128x128 w64x64 ks2 bk32", run_v8<128, 128, 64, 64, 2, 32>(a, s.reps));
-      rep("v8 128x128 w64x64 ks1 bk64", run_v8<128, 128, 64, 64, 1, 64>(a, s.reps));
-      rep("v8 128x128 w128x32 ks1 bk32", run_v8<128, 128, 128, 32, 1, 32>(a, s.reps));
+      rep("v1 128x128 w64x64 pf0 epi", run_v1<128, 128, 64, 64, 0, 1>(a, s.reps));
+      rep("v1 128x128 w64x64 pf3 epi", run_v1<128, 128, 64, 64, 3, 1>(a, s.reps));
+      rep("v1 128x64 w64x32 pf0 epi", run_v1<128, 64, 64, 32, 0, 1>(a, s.reps));
+      rep("v1 64x128 w32x64 pf0 epi", run_v1<64, 128, 32, 64, 0, 1>(a, s.reps));
+      rep("v1 128x128 w64x64 pf0 (again)", run_v1<128, 128, 64, 64, 0>(a, s.reps));
     }
   }
   return 0;
