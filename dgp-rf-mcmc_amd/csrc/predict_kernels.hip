@@ -531,6 +531,15 @@ constexpr int TW_ROWS = TWW * TR;  // rows per workgroup
 #ifndef DGPRF_TILE_G8MIX
 #define DGPRF_TILE_G8MIX 0  // 1: G8 RBF cos half on 16x16x4 tiles (measured slower: 241 vs 221 us)
 #endif
+#ifndef DGPRF_TILE_LEAN
+#define DGPRF_TILE_LEAN 1  // the lean instance (NOTMAX = 0) for models whose layers all have g, d <= 8
+#endif
+#ifndef DGPRF_TILE_LEAN_WAVES
+#define DGPRF_TILE_LEAN_WAVES 5  // waves per SIMD of the lean instance (NOTMAX = 0)
+#endif
+#ifndef DGPRF_TILE_LEAN_APHASE
+#define DGPRF_TILE_LEAN_APHASE 0  // the lean instance computes each chunk's A tile just before use
+#endif
 #ifndef DGPRF_TILE_G8
 #define DGPRF_TILE_G8 1  // layers with 2 <= g <= 8: F contraction on 4x4x1 MFMA blocks (no padding)
 #endif
@@ -547,7 +556,9 @@ __host__ __device__ inline TileLds tile_lds(const dgprf_plan_t& pl, int notmax, 
   for (int l = 0; l < pl.n_layers; ++l) gmax = pl.n_gp[l] > gmax ? pl.n_gp[l] : gmax;
   TileLds T;
   T.obuf = 16 * njo * TW_OST;               // njo float4 per thread: 16 Omega rows each
-  T.wbuf = 2 * 64 * tw_wst(notmax);         // [cos|sin][64 features][16 NOT + 4]
+  // [cos|sin][64 features][16 NOT + 4]; notmax = 0 (the lean instance: every layer g <= 8, d <= 8)
+  // [cos|sin][64 features][8] (G8) or [cos|sin][64] (g == 1)
+  T.wbuf = notmax == 0 ? 2 * 64 * 8 : 2 * 64 * tw_wst(notmax);
   T.o_off = 0;
   T.w_off = 2 * T.obuf;
   T.xin_st = wide0 ? 4 : round4(pl.d_in);  // wide0: layer 0 reads A_1, no input rows staged
@@ -565,7 +576,7 @@ __host__ __device__ inline TileLds tile_lds(const dgprf_plan_t& pl, int notmax, 
 // WST = 16 NOT + 4 (g == 1: raw [h][64]); feature rows >= R are zeroed while staging, and output
 // columns o >= g are never stored, so the fragment reads need neither masks nor clamps and all
 // their offsets are immediates.
-template <int NOT, bool RBF, bool G1, bool G8, int JW, int JO, int KS, int TPW>
+template <int NOT, bool RBF, bool G1, bool G8, int JW, int JO, int KS, int TPW, bool AP = true>
 __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
                                            const float* __restrict__ W,
                                            const float* __restrict__ om, float cl,
@@ -578,7 +589,7 @@ __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
   // two 4x4-block operands (o = i, 4 + i) are one ds_read_b64
   constexpr int WST = G8 ? 8 : tw_wst(NOT);
   constexpr bool REV = RBF && !DGPRF_PRECISE_TRIG_ON;
-  constexpr bool APHASE = DGPRF_TILE_APHASE && KS <= 2;
+  constexpr bool APHASE = AP && DGPRF_TILE_APHASE && KS <= 2;
   // the k-steps read Omega rows 0..4KS-1 of the staged block: all of them must be staged (rows >= d
   // as zeros) — LDS is not cleared between kernels, and 0 * stale NaN is NaN
   static_assert(4 * KS <= 16 * JO, "k-steps beyond the staged Omega rows");
@@ -872,9 +883,13 @@ __device__ unsigned long long g_pred_stamps[1 << 20];
 
 // WIDE: layer 0 reads a precomputed A_1 (separate instantiations keep the common kernels' registers);
 // g > 16 instances (NOTMAX > 1) are budgeted for 2 waves/SIMD: at 4 they spilled ~300 VGPRs.
+// NOTMAX = 0: the lean instance for models whose layers all have g <= 8 and d <= 8 (config 2): only
+// the G8 / g == 1 bodies with two k-steps, a G8-sized W ring, and a register budget for
+// DGPRF_TILE_LEAN_WAVES waves per SIMD (so a 1e5-row set fits about one round of workgroups).
 template <int NOTMAX, int JW, int JO, int TPW, bool WIDE>
 __global__ __launch_bounds__(TW_THREADS)
-__attribute__((amdgpu_waves_per_eu((TPW == 1 && NOTMAX == 1) ? DGPRF_TILE_WAVES : 2)))
+__attribute__((amdgpu_waves_per_eu(NOTMAX == 0 ? DGPRF_TILE_LEAN_WAVES
+                                               : ((TPW == 1 && NOTMAX == 1) ? DGPRF_TILE_WAVES : 2))))
 void k_forward_tiles(
     const dgprf_plan_t pl, const float* __restrict__ theta, const float* __restrict__ omega,
     const float* __restrict__ der, const float* __restrict__ X, const float* __restrict__ Y,
@@ -925,7 +940,15 @@ void k_forward_tiles(
       tile_layer<NT, RB, G1_, G8_, JW, JO, 4 * JO, TPW>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq,  \
                                                    wrow0, row_end, fout);                           \
   } while (0)
-    if (g == 1) {
+    if (NOTMAX == 0) {  // lean: g <= 8 and d <= 8 on every layer (host-checked)
+      if (g == 1) {
+        if (rbf) tile_layer<1, true, true, false, JW, JO, 2, TPW, DGPRF_TILE_LEAN_APHASE>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, row_end, fout);
+        else tile_layer<1, false, true, false, JW, JO, 2, TPW, DGPRF_TILE_LEAN_APHASE>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, row_end, fout);
+      } else {
+        if (rbf) tile_layer<1, true, false, true, JW, JO, 2, TPW, DGPRF_TILE_LEAN_APHASE>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, row_end, fout);
+        else tile_layer<1, false, false, true, JW, JO, 2, TPW, DGPRF_TILE_LEAN_APHASE>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, row_end, fout);
+      }
+    } else if (g == 1) {
       if (rbf) DGPRF_TL(1, true, true, false);
       else DGPRF_TL(1, false, true, false);
     } else if (DGPRF_TILE_G8 && g <= 8) {
@@ -1107,8 +1130,11 @@ hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const
       // >= 16 d / 256; the wide-g instances are compiled with JO = 2 only (host and kernel must
       // size the LDS ring identically)
       const int njo = (dmax <= 16 && njw <= 2) ? 1 : 2;
-      const int ntm = njw <= 2 ? 1 : (njw == 4 ? 2 : 4);
+      int ntm = njw <= 2 ? 1 : (njw == 4 ? 2 : 4);
       constexpr int tpw = DGPRF_TILE_TPW_DEFAULT;
+      bool lean = DGPRF_TILE_LEAN && DGPRF_TILE_G8 && !wide0 && tpw == 1 && njw == 1 && njo == 1;
+      for (int l = 0; l < pl.n_layers; ++l) lean = lean && pl.n_gp[l] <= 8 && pl.d[l] <= 8;
+      if (lean) ntm = 0;
       const TileLds T = tile_lds(pl, ntm, njo, tpw, wide0);
       dim3 tgrid((unsigned)((nr + TW_ROWS * tpw - 1) / (TW_ROWS * tpw)), pl.n_chains);
       const size_t tl = (size_t)T.total * sizeof(float);
@@ -1124,7 +1150,9 @@ hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const
     if (wide0) DGPRF_TILE_LAUNCH1(NM, J, JO, 1, true);                                             \
     else DGPRF_TILE_LAUNCH1(NM, J, JO, tpw, false);                                                \
   } while (0)
-      if (njw == 1) {
+      if (lean) {
+        DGPRF_TILE_LAUNCH1(0, 1, 1, 1, false);
+      } else if (njw == 1) {
         if (njo == 1) DGPRF_TILE_LAUNCH(1, 1, 1);
         else DGPRF_TILE_LAUNCH(1, 1, 2);
       } else if (njw == 2) {

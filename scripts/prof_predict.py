@@ -37,4 +37,5 @@ for _ in range(args.samples):
     acc.add_sample(build=False)
 ev1.record()
 torch.cuda.synchronize()
-print(f"predictive: {ev0.elapsed_time(ev1) / args.samples * 1e3:.1f} us/sample")
+print(f"predictive: {ev0.elapsed_time(ev1) / args.samples * 1e3:.1f} us/sample; "
+      f"finalize {acc.finalize()}")  # (the same numbers for every library build: a parity check)
