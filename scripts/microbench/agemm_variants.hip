@@ -1107,10 +1107,13 @@ int main() {
       a.gm = 0;
     } else {
       rep("v1 128x128 w64x64 pf0", run_v1<128, 128, 64, 64, 0>(a, s.reps));
-      rep("v1 128x128 w64x64 pf0 epi", run_v1<128, 128, 64, 64, 0, 1>(a, s.reps));
-      rep("v1 128x128 w64x64 pf3 epi", run_v1<128, 128, 64, 64, 3, 1>(a, s.reps));
-      rep("v1 128x64 w64x32 pf0 epi", run_v1<128, 64, 64, 32, 0, 1>(a, s.reps));
-      rep("v1 64x128 w32x64 pf0 epi", run_v1<64, 128, 32, 64, 0, 1>(a, s.reps));
+      rep("v1 64x64 w32x32 pf0", run_v1<64, 64, 32, 32, 0>(a, s.reps));
+      rep("v1 64x64 w32x32 pf3", run_v1<64, 64, 32, 32, 3>(a, s.reps));
+      a.gm = 8;
+      rep("v1 64x64 w32x32 pf3 xcd gm8", run_v1<64, 64, 32, 32, 3>(a, s.reps));
+      a.gm = 0;
+      rep("v1 64x128 w32x64 pf3", run_v1<64, 128, 32, 64, 3>(a, s.reps));
+      rep("v1 128x64 w64x32 pf3", run_v1<128, 64, 64, 32, 3>(a, s.reps));
       rep("v1 128x128 w64x64 pf0 (again)", run_v1<128, 128, 64, 64, 0>(a, s.reps));
     }
   }
