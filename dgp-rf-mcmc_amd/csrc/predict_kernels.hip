@@ -44,9 +44,9 @@ __host__ __device__ inline FwdLds fwd_lds(const dgprf_plan_t& pl, int nwr = NW, 
   L.xst = round4(dmax) + 1;
   L.ftst = round4(gmax) + 1;
   L.red_off = round4(tt * TR * L.xst);
-  // per-wave F partials [tt tiles x 16 rows][16 x output tiles]: sized for the model's widest
+  // per-wave F partials [tt tiles x 16 rows][16 x output tiles + 4]: sized for the model's widest
   // layer, so the 8- and 16-wave kernels fit two workgroups per CU
-  L.ft_off = L.red_off + nwr * tt * TR * (((gmax + 15) >> 4) << 4);
+  L.ft_off = L.red_off + nwr * tt * TR * ((((gmax + 15) >> 4) << 4) + 4);
   L.total = L.ft_off + round4(tt * TR * L.ftst);
   return L;
 }
@@ -56,7 +56,7 @@ struct FOut {
 };
 
 // One wave's F partial of one layer over its features (chunks wave, wave + NWR, ...), written to
-// red[wave][16][NOT*16].  Chunks go in groups of CG (4 for 4-wave tiles with NOT == 1, else 2): the group's Omega / W
+// red[wave][16][NOT*16 + 4].  Chunks go in groups of CG (4 for 4-wave tiles with NOT == 1, else 2): the group's Omega / W
 // fragments are loaded together (one L2 round trip per group instead of per chunk) and its chunks'
 // MFMA chains are independent; cos and sin products accumulate in separate chains.  G1 (g == 1):
 // the W^T Phi^T product is a per-lane dot product (VALU) reduced over the 4 lane groups, instead of
@@ -171,22 +171,22 @@ __device__ __forceinline__ void layer_partial(const float* __restrict__ om,
       }
     }
   }
-  constexpr int GP = NOT * 16;
-  float* redw = red + wave * TT * TR * GP;
+  // row stride GPS = 16 NOT + 4: conflict-free 16-byte row writes (16 NOT put every row on one bank)
+  constexpr int GPS = NOT * 16 + 4;
+  float* redw = red + wave * TT * TR * GPS;
 #pragma unroll
   for (int t = 0; t < TT; ++t) {
-    float* rt = redw + t * TR * GP;
+    float* rt = redw + t * TR * GPS;
     if (G1) {
       float v = dot[t];
       v += __shfl_xor(v, 16);
       v += __shfl_xor(v, 32);
-      if (lq == 0) rt[lr * GP] = v;
+      if (lq == 0) rt[lr * GPS] = v;
     } else {
       // acc[t][ot][r] = F partial[tile t, row lr][ot*16 + 4lq + r]
 #pragma unroll
       for (int ot = 0; ot < NOT; ++ot)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) rt[lr * GP + ot * 16 + 4 * lq + r] = acc[t][ot][r] + acs[t][ot][r];
+        *reinterpret_cast<f4*>(rt + lr * GPS + ot * 16 + 4 * lq) = acc[t][ot] + acs[t][ot];
     }
   }
 }
@@ -289,14 +289,14 @@ void k_forward_rows(
 #undef DGPRF_LP_ALL
 #undef DGPRF_LP
     }
-    const int GP = ((g + 15) >> 4) * 16;
+    const int GPS = ((g + 15) >> 4) * 16 + 4;  // (layer_partial's padded row stride)
     __syncthreads();
     float* out = fo.p[layer] ? fo.p[layer] + (int64_t)chain * n * g : nullptr;
     for (int e = threadIdx.x; e < TT * TR * g; e += blockDim.x) {
       const int r = e / g, o = e - r * g;
-      float v = red[r * GP + o];
+      float v = red[r * GPS + o];
 #pragma unroll
-      for (int w = 1; w < NWR; ++w) v += red[w * TT * TR * GP + r * GP + o];
+      for (int w = 1; w < NWR; ++w) v += red[w * TT * TR * GPS + r * GPS + o];
       ft[r * LD.ftst + o] = v;
       const int64_t b = row0 + r;
       if (out && b < row_end) out[b * g + o] = v;

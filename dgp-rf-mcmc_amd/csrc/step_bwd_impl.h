@@ -453,21 +453,20 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
   }
   if (dxw > 0) {
     // dxa[dt][r] = dX[row lr][dt*16 + 4lq + r]; sum the 4 waves in LDS, store the slice partial.
-    const int DP = ND * 16;
-    float* redw = red + wave * TR * DP;
+    // row stride DPS = 16 ND + 4: conflict-free 16-byte row writes (as the forward's F rows)
+    const int DPS = ND * 16 + 4;
+    float* redw = red + wave * TR * DPS;
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt)
-      if (dt < ND)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) redw[lr * DP + dt * 16 + 4 * lq + r] = dxa[dt][r];
+      if (dt < ND) *reinterpret_cast<f4*>(redw + lr * DPS + dt * 16 + 4 * lq) = dxa[dt];
     __syncthreads();
     float* dxp = a.dxout + (int64_t)chain * a.ws_cs + (int64_t)sl * B * dxw;
     for (int e = threadIdx.x; e < TR * dxw; e += blockDim.x) {
       const int r = e / dxw, k = e - r * dxw, b = row0 + r;
       if (b < B) {
-        float v = red[r * DP + k];
+        float v = red[r * DPS + k];
 #pragma unroll
-        for (int w = 1; w < NWB; ++w) v += red[w * TR * DP + r * DP + k];
+        for (int w = 1; w < NWB; ++w) v += red[w * TR * DPS + r * DPS + k];
         dxp[(int64_t)b * dxw + k] = v;
       }
     }

@@ -186,8 +186,8 @@ __device__ __forceinline__ float sum_slices(const float* __restrict__ p, int64_t
 }
 
 // LDS layout of one forward / backward workgroup of nwb waves (floats): X tile [TR][xst], the
-// backward's dF and Y tiles [TR][auxst], then `red` — the per-wave reduction rows (F [nwb][TR][GP]
-// in the forward, dX [nwb][TR][DP] in the backward; also the prologue's scratch slots) — then the
+// backward's dF and Y tiles [TR][auxst], then `red` — the per-wave reduction rows (F [nwb][TR][GP + 4]
+// in the forward, dX [nwb][TR][DP + 4] in the backward; also the prologue's scratch slots) — then the
 // backward's 64-feature W / Omega staging block when dPhi / dX need them.  Sized to the layer, so
 // small layers leave room for more resident workgroups (large minibatches).
 __host__ __device__ inline void step_lds(LayerK& a, int& total, int nwb, bool bwd, bool dphi) {
@@ -197,7 +197,8 @@ __host__ __device__ inline void step_lds(LayerK& a, int& total, int nwb, bool bw
   a.auxst = g + 1;
   a.red_off = a.aux_off + (bwd ? 2 * round4(TR * a.auxst) : 0);  // dF tile + Y tile
   const int np = 64 * nwb < 512 ? 64 * nwb : 512;       // prologue owners (scratch: 2 np slots)
-  const int gp16 = (g + 15) / 16 * 16, dp16 = (a.dxw + 15) / 16 * 16;
+  // reduction rows padded by 4 floats (conflict-free 16-byte row writes)
+  const int gp16 = (g + 15) / 16 * 16 + 4, dp16 = (a.dxw + 15) / 16 * 16 + 4;
   const int rows = nwb * TR * (bwd ? dp16 : gp16);
   a.stg_off = a.red_off + round4(rows > 2 * np ? rows : 2 * np);
   if (bwd && dphi) {  // backward: the workgroup's 64-feature block of W_l ([2][64*g]), Omega_l ([64][OST])

@@ -87,18 +87,19 @@ __global__ __launch_bounds__(64 * NWB) void k_step_fwd(const LayerK a) {
     }
   }
   DGPRF_STAMP(stamp_base, 7);
-  // acc[ot][r] = F[row lr][ot*16 + 4lq + r]; sum the 4 waves' feature chunks in LDS.
-  constexpr int GP = NOT * 16;
-  float* redw = red + wave * TR * GP;
+  // acc[ot][r] = F[row lr][ot*16 + 4lq + r]; sum the 4 waves' feature chunks in LDS.  Row stride
+  // GPS = 16 NOT + 4: the 16-byte row writes of 8 lanes (one LDS cycle group) start 4 banks apart
+  // (a stride of 16 NOT put all 16 rows on one bank: 16-way conflicts)
+  constexpr int GPS = NOT * 16 + 4;
+  float* redw = red + wave * TR * GPS;
   if (G1) {
     acc1 += __shfl_xor(acc1, 16);
     acc1 += __shfl_xor(acc1, 32);
-    if (lq == 0) redw[lr * GP] = acc1;
+    if (lq == 0) redw[lr * GPS] = acc1;
   } else {
 #pragma unroll
     for (int ot = 0; ot < NOT; ++ot)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) redw[lr * GP + ot * 16 + 4 * lq + r] = acc[ot][r] + acs[ot][r];
+      *reinterpret_cast<f4*>(redw + lr * GPS + ot * 16 + 4 * lq) = acc[ot] + acs[ot];
   }
   DGPRF_STAMP(stamp_base, 3);
   __syncthreads();
@@ -106,9 +107,9 @@ __global__ __launch_bounds__(64 * NWB) void k_step_fwd(const LayerK a) {
   for (int e = threadIdx.x; e < TR * g; e += blockDim.x) {
     const int r = e / g, o = e - r * g, b = row0 + r;
     if (b < B) {
-      float v = red[r * GP + o];
+      float v = red[r * GPS + o];
 #pragma unroll
-      for (int w = 1; w < NWB; ++w) v += red[w * TR * GP + r * GP + o];
+      for (int w = 1; w < NWB; ++w) v += red[w * TR * GPS + r * GPS + o];
       fp[(int64_t)b * g + o] = v;
     }
   }
