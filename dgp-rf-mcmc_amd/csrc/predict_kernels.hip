@@ -576,13 +576,23 @@ __host__ __device__ inline TileLds tile_lds(const dgprf_plan_t& pl, int notmax, 
 // WST = 16 NOT + 4 (g == 1: raw [h][64]); feature rows >= R are zeroed while staging, and output
 // columns o >= g are never stored, so the fragment reads need neither masks nor clamps and all
 // their offsets are immediates.
-template <int NOT, bool RBF, bool G1, bool G8, int JW, int JO, int KS, int TPW, bool AP = true>
+// OPQ: the lane index re-read behind an empty asm, so this layer's per-lane LDS offsets are computed
+// here and not hoisted above the caller's layer loop (where, live through every layer, they pushed
+// the lean instance past its 96-VGPR budget into scratch)
+template <int NOT, bool RBF, bool G1, bool G8, int JW, int JO, int KS, int TPW, bool AP = true,
+          bool OPQ = false>
 __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
                                            const float* __restrict__ W,
                                            const float* __restrict__ om, float cl,
                                            const TileLds& T, float* smem, float* xin, float* ftw,
                                            int lr, int lq, int64_t wrow0, int64_t n, float* fout,
                                            const float* __restrict__ arow0 = nullptr) {
+  if (OPQ) {
+    int ln = (int)threadIdx.x & 63;
+    asm volatile("" : "+v"(ln));
+    lr = ln & 15;
+    lq = ln >> 4;
+  }
   // arow0 (wide first layer): A_1 rows of this wave's tiles, [row][R] (k_step_agemm); the Omega
   // staging and A-tile MFMAs are skipped and A is read straight into the accumulator layout
   // G8 (2 <= g <= 8): W rows of 8 with the columns interleaved as 2 (o & 3) + (o >> 2), so a lane's
@@ -595,7 +605,8 @@ __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
   static_assert(4 * KS <= 16 * JO, "k-steps beyond the staged Omega rows");
   const int d = pl.d[layer], R = pl.n_rf[layer], g = pl.n_gp[layer];
   const int gp = layer > 0 ? pl.n_gp[layer - 1] : 0;
-  const int tid = threadIdx.x;
+  int tid = threadIdx.x;
+  if (OPQ) asm volatile("" : "+v"(tid));
   const int gmag = (1048576 + g - 1) / g;  // floor(e / g) = (e * gmag) >> 20 for e < 4096
   // x fragments of the A = Omega^T x contraction: xf[t][ks] = X_l[tile t, row lr][4ks + lq]
   float xf[TPW][KS];
@@ -942,11 +953,11 @@ void k_forward_tiles(
   } while (0)
     if (NOTMAX == 0) {  // lean: g <= 8 and d <= 8 on every layer (host-checked)
       if (g == 1) {
-        if (rbf) tile_layer<1, true, true, false, JW, JO, 2, TPW, DGPRF_TILE_LEAN_APHASE>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, row_end, fout);
-        else tile_layer<1, false, true, false, JW, JO, 2, TPW, DGPRF_TILE_LEAN_APHASE>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, row_end, fout);
+        if (rbf) tile_layer<1, true, true, false, JW, JO, 2, TPW, DGPRF_TILE_LEAN_APHASE, true>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, row_end, fout);
+        else tile_layer<1, false, true, false, JW, JO, 2, TPW, DGPRF_TILE_LEAN_APHASE, true>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, row_end, fout);
       } else {
-        if (rbf) tile_layer<1, true, false, true, JW, JO, 2, TPW, DGPRF_TILE_LEAN_APHASE>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, row_end, fout);
-        else tile_layer<1, false, false, true, JW, JO, 2, TPW, DGPRF_TILE_LEAN_APHASE>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, row_end, fout);
+        if (rbf) tile_layer<1, true, false, true, JW, JO, 2, TPW, DGPRF_TILE_LEAN_APHASE, true>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, row_end, fout);
+        else tile_layer<1, false, false, true, JW, JO, 2, TPW, DGPRF_TILE_LEAN_APHASE, true>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, row_end, fout);
       }
     } else if (g == 1) {
       if (rbf) DGPRF_TL(1, true, true, false);
