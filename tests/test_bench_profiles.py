@@ -29,8 +29,9 @@ def test_step_flops_config2():
 def test_roofline_frac_from_live_duration():
     roof = _line()["roofline"]
     frac = roof["flops_per_launch"] / (roof["avg_launch_us"] * 1e-6) / bench.FP32_MFMA_PEAK
-    assert roof["frac"] == pytest.approx(frac, rel=1e-4)
-    assert roof["achieved"] == pytest.approx(frac * bench.FP32_MFMA_PEAK / 1e12, rel=1e-4)
+    # the line rounds avg_launch_us to 1 ns (~3e-4 of a ~4 us launch); frac is taken before rounding
+    assert roof["frac"] == pytest.approx(frac, rel=1e-3)
+    assert roof["achieved"] == pytest.approx(frac * bench.FP32_MFMA_PEAK / 1e12, rel=1e-3)
 
 
 def test_committed_trace_agrees_with_live():
