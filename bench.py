@@ -37,7 +37,7 @@ HBM_PEAK = 8.0e12           # MI355X_MICROARCH.md: HBM3E spec (B/s)
 # MI355X_MICROARCH.md per-instruction table: v_sin_f32 / v_cos_f32 issue 8 cycles per 64-lane wave
 # instruction on a SIMD; 256 CUs x 4 SIMDs at the 2.4 GHz peak clock
 TRANS_PER_S = 1024 * 64 / 8 * 2.4e9
-PROFILES = os.path.join(ROOT, "profiles", "r04")   # this round's committed rocprofv3 evidence
+PROFILES = os.path.join(ROOT, "profiles", "r05")   # this round's committed rocprofv3 evidence
 
 CFG = dict(L=3, n_rf=1024, n_gp=[8, 8, 1], D=8, N=1_000_000, B=200, N_test=100_000,
            variance=0.1, lr=0.01, beta=0.9, T=1.0)
@@ -145,7 +145,7 @@ def _short(name):
 
 def pmc_traffic(prefix):
     """HBM-side bytes per launch of the kernels named `prefix...` (dispatch-weighted mean), from the
-    committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes (profiles/r04/pmc_traffic.json, made by
+    committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes (profiles/r05/pmc_traffic.json, made by
     scripts/gpu_profile_round.sh; FETCH doubled per MI355X_MICROARCH.md §HBM).  None if absent."""
     path = os.path.join(PROFILES, "pmc_traffic.json")
     if not os.path.exists(path):
@@ -159,7 +159,7 @@ def pmc_traffic(prefix):
 
 def rocprof_avg_us(prefix, fname="kernel_stats_bench.csv"):
     """Dispatch-weighted average duration (us) of the kernels named `prefix<...>` in the committed
-    rocprofv3 --kernel-trace --stats summary of this bench (profiles/r04/kernel_stats_bench.csv);
+    rocprofv3 --kernel-trace --stats summary of this bench (profiles/r05/kernel_stats_bench.csv);
     None if absent.  Traced durations include each dispatch's own launch overhead."""
     import csv
     path = os.path.join(PROFILES, fname)
@@ -232,7 +232,13 @@ def bench_config(cfg, dev, rank, world, barrier_sync, max_over_ranks, steps):
     for _ in range(S):
         acc.add_sample(build=False)
     ev1.record()
+    # the config's predictive ends with the accumulator all-gather over the ranks (RCCL over xGMI
+    # under nccl) and the device log-sum-exp combine (utils_training.py:79-85): inside the region
     barrier_sync()
+    t1 = time.perf_counter()
+    ll, _ = acc.finalize(y_std=1.0)
+    barrier_sync()
+    t_fin = max_over_ranks(time.perf_counter() - t1)
     t_p = max_over_ranks(time.perf_counter() - t0)
     k_ms = ev0.elapsed_time(ev1) / S
     fp = pred_flops(nt, d, R, P, g)
@@ -243,11 +249,57 @@ def bench_config(cfg, dev, rank, world, barrier_sync, max_over_ranks, steps):
            "step_mflop": round((sum(fwd_f) + sum(bwd_f)) / 1e6, 2),
            "step_mfma_frac": round((sum(fwd_f) + sum(bwd_f)) / (t_s / steps) / FP32_MFMA_PEAK, 4),
            "predictive_samples_per_s": round(world * S / t_p, 3), "n_test": nt,
+           "predictive_finalize_ms": round(t_fin * 1e3, 3),
+           "predictive_finalize": f"all-gather of the [chains, {nt}] (max, sum, se) accumulators "
+                                  f"over {world} rank(s) + device LSE combine, inside the timed "
+                                  "predictive region",
+           "test_loglik": round(ll, 5),
            "predictive_kernel_ms": round(k_ms, 3),
            "predictive_mfma_frac": round(fp / (k_ms * 1e-3) / FP32_MFMA_PEAK, 4),
            "a1_gemm": a1}
     del m, acc, X, Y, Xt, Yt
     torch.cuda.empty_cache()
+    return out
+
+
+def eager_api(model, X, Y, N_, B, calls=2000, n_batches=50):
+    """The drop-in per-call path the reference's driver runs (experiments/utils_training.py:45-61):
+    one model.sgmcmc_update(x, y, N, ...) call per minibatch (models/dgp.py:184-216), each a
+    Python -> torch-op -> C-ABI call launching the step's kernels; minibatches device-resident
+    (slices of the HBM dataset) and host numpy arrays copied per call, as a tf.data loader hands
+    them over.  Also precond_update(ds, N, K_batches=32) (run every epoch by the reference,
+    experiments/utils_training.py:42).  The model's momenta and masses are restored afterwards."""
+    eng = model._engine
+    keep = (eng.theta.clone(), eng.mom.clone(), eng.mass.clone(), int(eng.step_ctr))
+    dev_b = [(X[i * B:(i + 1) * B], Y[i * B:(i + 1) * B]) for i in range(n_batches)]
+    host_b = [(x.cpu().numpy(), y.cpu().numpy()) for x, y in dev_b]
+    kw = dict(lr=CFG["lr"], momentum_decay=CFG["beta"], temperature=CFG["T"])
+    out = {}
+    for name, batches in (("device_batches", dev_b), ("host_numpy_batches", host_b)):
+        for i in range(50):
+            model.sgmcmc_update(*batches[i % n_batches], N_, **kw)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(calls):
+            model.sgmcmc_update(*batches[i % n_batches], N_, **kw)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        out[name] = {"steps_per_s": round(calls / dt, 1), "us_per_call": round(dt * 1e6 / calls, 2),
+                     "calls": calls}
+    ds = [dev_b[i % n_batches] for i in range(32)]
+    model.precond_update(ds, N_, K_batches=32)  # warm (workspace / scratch allocation)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    model.precond_update(ds, N_, K_batches=32)
+    torch.cuda.synchronize()
+    out["precond_update_k32_ms"] = round((time.perf_counter() - t0) * 1e3, 3)
+    eng.theta.copy_(keep[0])
+    eng.mom.copy_(keep[1])
+    eng.mass.copy_(keep[2])
+    eng.step_ctr.fill_(keep[3])
+    out["method"] = ("model.sgmcmc_update per call, B=200 config-2 minibatches (50 distinct, "
+                     "cycled), wall time over `calls` calls closed by a synchronize; Omega built "
+                     "only when stale; precond_update: 32 gradient minibatches + Welford + masses")
     return out
 
 
@@ -356,6 +408,7 @@ def main():
     ap.add_argument("--other-configs", type=int, default=1)
     ap.add_argument("--other-steps", type=int, default=1000)
     ap.add_argument("--b-sweep", type=int, default=1)
+    ap.add_argument("--eager-calls", type=int, default=2000)
     args = ap.parse_args()
 
     # DGPRF_BENCH_BACKEND=gloo (with ranks sharing a GPU: local % device_count) rehearses the N > 1
@@ -473,16 +526,17 @@ def main():
     upd_bytes = 4 * pl.w_total * (pl.n_row_tiles + 2 + 2 + 2)  # gW partials + theta/mom r/w
     dom = max(per_name, key=lambda k: per_name[k][0] * per_name[k][2])
     ms_dom, fl_dom, _ = per_name[dom]
-    # duration per launch (`achieved` / `frac`): the dominant kernel's share of this run's timed
-    # region, live — the hipEvent step time over the K timed steps, split over the step's kernels
-    # in proportion to their event-pair times (each pair holds its kernel and one dependent-launch
-    # boundary), per launch.  The in-kernel span (pair minus an empty pair) is reported beside it
-    # (live_in_kernel_us), and the committed rocprofv3 kernel trace of the same command (profiles/
-    # r04/) as the cross-check (rocprof_avg_launch_us)
     rp_us = rocprof_avg_us(dom)
     n_dom = per_name[dom][2]
     dom_pairs = inflow[:Lk] if dom == "k_step_fwd" else inflow[Lk:2 * Lk]
-    use_us = step_ms_dev * 1e3 * sum(dom_pairs) / sum(inflow) / n_dom
+    share_us = step_ms_dev * 1e3 * sum(dom_pairs) / sum(inflow) / n_dom
+    live_us = ms_dom * 1e3
+    # duration per launch (`achieved` / `frac`): the committed rocprofv3 kernel trace of this bench
+    # (profiles/rNN/kernel_stats_bench.csv, dispatch-weighted mean over the kernel's instances), so
+    # `frac` recomputes from that file; the live in-kernel span measured here (hipEvent pair on the
+    # launch stream minus an empty pair) is reported beside it and must agree within 15 %
+    # (tests/test_bench_profiles.py).  Without a committed trace the live span is used.
+    use_us = rp_us if rp_us else live_us
     n_launch = 2 * len(d) + 1
     bnd_us = launch_boundary_us(dev)
     rel = os.path.relpath(PROFILES, ROOT)
@@ -494,20 +548,22 @@ def main():
             "traffic_source": f"{rel}/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE "
                               "passes of this bench; bytes per launch incl. Infinity-Cache hits)",
             "avg_launch_us": round(use_us, 3),
-            "duration_source": "live: the kernel's share of the timed region's hipEvent step time "
-                               "(step_us_events), split over the step's 2L+1 kernels by their "
-                               "event-pair times (dgprf_profile_step, --profile-reps real steps on "
-                               "the launch stream), per launch: kernel + its launch boundary",
-            "live_in_kernel_us": round(ms_dom * 1e3, 3),
-            "live_in_kernel_method": "event pair around the kernel minus an empty pair: the span "
-                                     "inside the kernel, without its launch boundary",
+            "duration_source": (f"{rel}/kernel_stats_bench.csv: rocprofv3 --kernel-trace --stats "
+                                "of this bench, dispatch-weighted mean duration of the kernel's "
+                                "instances (a traced duration also holds the dispatch's launch and "
+                                "the tracer's completion signal, DESIGN.md §5)" if rp_us else
+                                "live in-kernel span (no committed trace)"),
+            "live_in_kernel_us": round(live_us, 3),
+            "live_frac": round(fl_dom / (live_us * 1e-6) / FP32_MFMA_PEAK, 8),
+            "live_in_kernel_method": "hipEvent pair around the kernel on its launch stream minus an "
+                                     "empty pair (dgprf_profile_step, --profile-reps real steps): "
+                                     "the span inside the kernel, without its launch boundary",
+            "live_share_us": round(share_us, 3),
+            "live_share_method": "the timed region's hipEvent step time split over the step's "
+                                 "kernels by their event-pair times, per launch (a lower bound "
+                                 "where the pairs overlap the boundaries)",
             "flops_per_launch": int(fl_dom),
             "rocprof_avg_launch_us": rp_us,
-            "rocprof_frac": (round(fl_dom / (rp_us * 1e-6) / FP32_MFMA_PEAK, 8) if rp_us else None),
-            "rocprof_source": (f"{rel}/kernel_stats_bench.csv: rocprofv3 --kernel-trace --stats of "
-                               "this bench, dispatch-weighted average of the kernel's instances; a "
-                               "traced duration also holds the dispatch's launch and the tracer's "
-                               "completion signal (DESIGN.md §5)" if rp_us else None),
             "launch_floor": {"launches_per_step": n_launch, "boundary_us": round(bnd_us, 3),
                              "floor_us_per_step": round(n_launch * bnd_us, 3),
                              "steps_per_s_ceiling": round(1e6 / (n_launch * bnd_us), 1),
@@ -538,6 +594,9 @@ def main():
                      "frac_of_sample_time": round(n_trans / TRANS_PER_S / (pred_kernel_ms * 1e-3), 4),
                      "rate_source": "MI355X_MICROARCH.md: v_sin_f32 / v_cos_f32 8 issue cycles per "
                                     "wave instruction, 1024 SIMDs, 2.4 GHz"}}
+
+    # ---------------- the reference driver's per-call path (extra, not `value`)
+    eager = eager_api(model, X, Y, N_, B, calls=args.eager_calls) if args.eager_calls > 0 else None
 
     # ---------------- many chains per GPU (aggregate chain-steps/s; extra, not `value`)
     multi = None
@@ -621,7 +680,7 @@ def main():
                            "test_loglik": round(ll, 6), "test_rmse": round(rmse, 6),
                            "ms_per_sample": round(t_pred * 1e3 / args.pred_samples, 4)},
             "roofline": roof, "roofline_predictive": roof_pred, "cpu_baseline": cpu,
-            "multi_chain": multi, "full_bayes": full_bayes, "other_configs": other or None,
+            "eager_api": eager, "multi_chain": multi, "full_bayes": full_bayes, "other_configs": other or None,
             "b_sweep": sweep,
             "device": torch.cuda.get_device_name(dev),
         }

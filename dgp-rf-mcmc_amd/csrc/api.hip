@@ -284,6 +284,9 @@ int dgprf_plan_init(dgprf_plan_t* pl) {
     pl->a0_off = ws;
     ws = align4(ws + 2 * (int64_t)((B + 31) / 32 * 32) * pl->n_rf[0]);
   }
+  // the row-group / row-wave backward kernels address a chain's workspace with 32-bit buffer
+  // offsets: refuse the plan here rather than failing every step at launch
+  if (pl->rt_per_group > 1 && ws >= ((int64_t)1 << 29)) return DGPRF_E_SHAPE;
   pl->ws_chain = ws;
   pl->ws_total = ws * pl->n_chains;
   pl->initialised = 1;

@@ -19,12 +19,8 @@
 namespace {
 
 constexpr int NW = DGPRF_WAVES;
-#ifndef DGPRF_ROWS16_WPE
-#define DGPRF_ROWS16_WPE 8  // waves per SIMD the 16-wave row kernel is budgeted for (8: two per CU)
-#endif
-#ifndef DGPRF_ROWS16_CG
-#define DGPRF_ROWS16_CG 1  // 16-feature chunks per fragment-load group in the 16-wave row kernel
-#endif
+constexpr int ROWS16_WPE = 8;  // waves per SIMD the 16-wave row kernel is budgeted for (two per CU)
+constexpr int ROWS16_CG = 1;   // 16-feature chunks per fragment-load group in the 16-wave row kernel
 constexpr int TR = DGPRF_TILE_ROWS;
 constexpr float LOG_2PI = 1.8378770664093453f;
 
@@ -71,7 +67,7 @@ __device__ __forceinline__ void layer_partial(const float* __restrict__ om,
                                               float cl, const float* xs, int xst, float* red,
                                               int wave, int lr, int lq,
                                               const float* __restrict__ arow = nullptr) {
-  constexpr int CG = NWR >= 16 ? DGPRF_ROWS16_CG : ((NWR >= 8 || NOT > 1) ? 2 : 4);
+  constexpr int CG = NWR >= 16 ? ROWS16_CG : ((NWR >= 8 || NOT > 1) ? 2 : 4);
   static_assert(NKS == 2 || NKS == 3 || NKS == 4 || NKS == 8, "k-step bucket");
   // TT tiles per workgroup (rows t * 16 + lr): every Omega / W fragment serves all of them
   static_assert(TT == 1 || SMALLD, "two-tile workgroups: register-fragment path only");
@@ -203,7 +199,7 @@ __device__ __forceinline__ void layer_partial(const float* __restrict__ om,
 // CU (explicit DGPRF_FWD_ROWS16 past one tile per CU), 4 when each CU holds one workgroup (the
 // 16-wave kernel then keeps its fragments in registers instead of spilling).
 template <bool SMALLD, int NOTMAX, int NWR, int TT = 1,
-          int WPE = (NWR == 16 ? DGPRF_ROWS16_WPE : (NWR == 8 ? 4 : 1))>
+          int WPE = (NWR == 16 ? ROWS16_WPE : (NWR == 8 ? 4 : 1))>
 __global__ __launch_bounds__(64 * NWR)
 __attribute__((amdgpu_waves_per_eu(TT > 1 ? 4 : WPE)))
 void k_forward_rows(
@@ -508,41 +504,21 @@ __global__ __launch_bounds__(256) void k_prior_w(const dgprf_plan_t pl,
 //     per block;
 //   * the layer output F (16 x g per wave) stays in the wave's LDS tile and is the next layer's
 //     input; dataset columns ([F | X], utils.py:42) come from the wave's X rows, loaded once.
-#ifndef DGPRF_TILE_WG_WAVES
 // waves per workgroup (4 waves = 4 SIMDs).  16 (one workgroup per CU) makes the per-block barrier
 // keep the 4 waves of each SIMD in step — otherwise oldest-first issue arbitration starves the
 // younger waves and the last ones finish alone — but measured no faster at N_t = 1e5 (lockstep
 // phases overlap MFMA and VALU worse, and 1.5 rounds of 16-tile workgroups leave half the CUs idle
 // in the second); DESIGN.md §4.
-#define DGPRF_TILE_WG_WAVES 4
-#endif
-constexpr int TWW = DGPRF_TILE_WG_WAVES;
+constexpr int TWW = 4;
 constexpr int TW_THREADS = 64 * TWW;
 constexpr int TW_ROWS = TWW * TR;  // rows per workgroup
-#ifndef DGPRF_TILE_WAVES
-#define DGPRF_TILE_WAVES 4  // waves per SIMD the register budget must allow (latency hiding)
-#endif
-#ifndef DGPRF_TILE_TPW_DEFAULT
-#define DGPRF_TILE_TPW_DEFAULT 1  // 16-row tiles per wave (2: two chains per wave, but 186 VGPRs -> 2 waves/SIMD, slower)
-#endif
-#ifndef DGPRF_TILE_APHASE
-#define DGPRF_TILE_APHASE 1  // issue a block's four A-tile chains before its trig / F work
-#endif
-#ifndef DGPRF_TILE_G8MIX
-#define DGPRF_TILE_G8MIX 0  // 1: G8 RBF cos half on 16x16x4 tiles (measured slower: 241 vs 221 us)
-#endif
-#ifndef DGPRF_TILE_LEAN
-#define DGPRF_TILE_LEAN 1  // the lean instance (NOTMAX = 0) for models whose layers all have g, d <= 8
-#endif
-#ifndef DGPRF_TILE_LEAN_WAVES
-#define DGPRF_TILE_LEAN_WAVES 5  // waves per SIMD of the lean instance (NOTMAX = 0)
-#endif
-#ifndef DGPRF_TILE_LEAN_APHASE
-#define DGPRF_TILE_LEAN_APHASE 0  // the lean instance computes each chunk's A tile just before use
-#endif
-#ifndef DGPRF_TILE_G8
-#define DGPRF_TILE_G8 1  // layers with 2 <= g <= 8: F contraction on 4x4x1 MFMA blocks (no padding)
-#endif
+constexpr int TILE_WAVES = 4;       // waves per SIMD the register budget must allow (latency hiding)
+constexpr int TILE_TPW_DEFAULT = 1; // 16-row tiles per wave (2: two chains per wave, but 186 VGPRs ->
+                                    // 2 waves/SIMD, slower)
+constexpr bool TILE_APHASE = true;  // issue a block's four A-tile chains before its trig / F work
+constexpr int TILE_LEAN_WAVES = 5;  // waves per SIMD of the lean instance (NOTMAX = 0, every layer
+                                    // g, d <= 8); it computes each chunk's A tile just before use
+                                    // (the A-phase there measured slower: 225 vs 213 us)
 constexpr int TW_OST = 80;        // LDS row stride of a staged Omega block (conflict-free reads)
 __host__ __device__ constexpr int tw_wst(int notm) { return 16 * notm + 4; }  // W row stride
 
@@ -599,7 +575,7 @@ __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
   // two 4x4-block operands (o = i, 4 + i) are one ds_read_b64
   constexpr int WST = G8 ? 8 : tw_wst(NOT);
   constexpr bool REV = RBF && !DGPRF_PRECISE_TRIG_ON;
-  constexpr bool APHASE = AP && DGPRF_TILE_APHASE && KS <= 2;
+  constexpr bool APHASE = AP && TILE_APHASE && KS <= 2;
   // the k-steps read Omega rows 0..4KS-1 of the staged block: all of them must be staged (rows >= d
   // as zeros) — LDS is not cleared between kernels, and 0 * stale NaN is NaN
   static_assert(4 * KS <= 16 * JO, "k-steps beyond the staged Omega rows");
@@ -701,8 +677,6 @@ __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
     const float* wsb = smem + T.w_off + buf * T.wbuf;
     const float* osb = smem + T.o_off + buf * T.obuf + lq * TW_OST + lr;
     const float* wl = wsb + (G1 ? 4 * lq : (G8 ? 4 * lq * WST + 2 * (lr & 3) : 4 * lq * WST + lr));
-    // G8 + MIX: W^T operand of the 16x16x4 cos tiles, row o = lr (interleaved column)
-    const float* wl16 = wsb + 4 * lq * WST + 2 * (lr & 3) + ((lr >> 2) & 1);
     // A[tile t, row lr][feature fb + 16c + 4lq + r]; the Omega / W fragments serve every tile.
     // APHASE: the four chunks' A tiles are issued together first (independent MFMA chains, so their
     // dependent latency overlaps), and the trig + F contraction of chunk c follows.
@@ -777,28 +751,18 @@ __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
           }
       } else if (G8) {
         // 4x4x1 blocks: block b = 4 lq + (lr >> 2) covers rows 4 (b & 3) + j and feature 4 lq + r;
-        // A = W[feature][4h + (lr & 3)], B = this lane's cos / sin value.
-        // MIX (RBF): the cos half stays on 16x16x4 tiles (rows o >= 8 of the A operand read other
-        // columns; their outputs are never used) — 4x4 blocks are cheap in the matrix pipe but hold
-        // the SIMD's issue port, so the two forms are split to balance the two limits.
-        constexpr bool MIX = RBF && DGPRF_TILE_G8MIX;
+        // A = W[feature][4h + (lr & 3)], B = this lane's cos / sin value.  (The cos half on 16x16x4
+        // tiles instead measured slower: 241 vs 221 us per config-2 sample.)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           typedef float f2v __attribute__((ext_vector_type(2)));
-          f2v wc = {0.f, 0.f};
-          float wc16 = 0.f;
-          if (MIX) wc16 = wl16[(16 * c + r) * WST];
-          else wc = *reinterpret_cast<const f2v*>(wl + (16 * c + r) * WST);
+          const f2v wc = *reinterpret_cast<const f2v*>(wl + (16 * c + r) * WST);
           f2v wsn = {0.f, 0.f};
           if (RBF) wsn = *reinterpret_cast<const f2v*>(wl + (64 + 16 * c + r) * WST);
 #pragma unroll
           for (int t = 0; t < TPW; ++t) {
-            if (MIX) {
-              acc[t][0] = mfma16(wc16, p0[t][r], acc[t][0]);
-            } else {
-              a8[t][0] = mfma4(wc[0], p0[t][r], a8[t][0]);
-              a8[t][1] = mfma4(wc[1], p0[t][r], a8[t][1]);
-            }
+            a8[t][0] = mfma4(wc[0], p0[t][r], a8[t][0]);
+            a8[t][1] = mfma4(wc[1], p0[t][r], a8[t][1]);
             if (RBF) {
               s8[t][0] = mfma4(wsn[0], p1[t][r], s8[t][0]);
               s8[t][1] = mfma4(wsn[1], p1[t][r], s8[t][1]);
@@ -840,7 +804,6 @@ __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
       }
     } else if (G8) {
       // sum the four feature groups (lanes lr, lr + 16, lr + 32, lr + 48)
-      constexpr bool MIX = RBF && DGPRF_TILE_G8MIX;
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -849,9 +812,7 @@ __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
           v += __shfl_xor(v, 16);
           v += __shfl_xor(v, 32);
           const int o = 4 * h + i;
-          // MIX: the 16x16x4 cos tile holds F^T[o = 4 lq + i][row lr] in lane group lq = h
-          if ((MIX ? lq == h : lq == 0) && o < g) {
-            if (MIX) v += acc[t][0][i];
+          if (lq == 0 && o < g) {
             v *= cl;
             ftw[row * T.ftst + o] = v;
             if (fout && b < n) fout[b * g + o] = v;
@@ -896,11 +857,11 @@ __device__ unsigned long long g_pred_stamps[1 << 20];
 // g > 16 instances (NOTMAX > 1) are budgeted for 2 waves/SIMD: at 4 they spilled ~300 VGPRs.
 // NOTMAX = 0: the lean instance for models whose layers all have g <= 8 and d <= 8 (config 2): only
 // the G8 / g == 1 bodies with two k-steps, a G8-sized W ring, and a register budget for
-// DGPRF_TILE_LEAN_WAVES waves per SIMD (so a 1e5-row set fits about one round of workgroups).
+// TILE_LEAN_WAVES waves per SIMD (so a 1e5-row set fits about one round of workgroups).
 template <int NOTMAX, int JW, int JO, int TPW, bool WIDE>
 __global__ __launch_bounds__(TW_THREADS)
-__attribute__((amdgpu_waves_per_eu(NOTMAX == 0 ? DGPRF_TILE_LEAN_WAVES
-                                               : ((TPW == 1 && NOTMAX == 1) ? DGPRF_TILE_WAVES : 2))))
+__attribute__((amdgpu_waves_per_eu(NOTMAX == 0 ? TILE_LEAN_WAVES
+                                               : ((TPW == 1 && NOTMAX == 1) ? TILE_WAVES : 2))))
 void k_forward_tiles(
     const dgprf_plan_t pl, const float* __restrict__ theta, const float* __restrict__ omega,
     const float* __restrict__ der, const float* __restrict__ X, const float* __restrict__ Y,
@@ -953,16 +914,16 @@ void k_forward_tiles(
   } while (0)
     if (NOTMAX == 0) {  // lean: g <= 8 and d <= 8 on every layer (host-checked)
       if (g == 1) {
-        if (rbf) tile_layer<1, true, true, false, JW, JO, 2, TPW, DGPRF_TILE_LEAN_APHASE, true>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, row_end, fout);
-        else tile_layer<1, false, true, false, JW, JO, 2, TPW, DGPRF_TILE_LEAN_APHASE, true>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, row_end, fout);
+        if (rbf) tile_layer<1, true, true, false, JW, JO, 2, TPW, false, true>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, row_end, fout);
+        else tile_layer<1, false, true, false, JW, JO, 2, TPW, false, true>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, row_end, fout);
       } else {
-        if (rbf) tile_layer<1, true, false, true, JW, JO, 2, TPW, DGPRF_TILE_LEAN_APHASE, true>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, row_end, fout);
-        else tile_layer<1, false, false, true, JW, JO, 2, TPW, DGPRF_TILE_LEAN_APHASE, true>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, row_end, fout);
+        if (rbf) tile_layer<1, true, false, true, JW, JO, 2, TPW, false, true>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, row_end, fout);
+        else tile_layer<1, false, false, true, JW, JO, 2, TPW, false, true>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, row_end, fout);
       }
     } else if (g == 1) {
       if (rbf) DGPRF_TL(1, true, true, false);
       else DGPRF_TL(1, false, true, false);
-    } else if (DGPRF_TILE_G8 && g <= 8) {
+    } else if (g <= 8) {
       if (rbf) DGPRF_TL(1, true, false, true);
       else DGPRF_TL(1, false, false, true);
     } else if (NOT == 1) {
@@ -1142,8 +1103,8 @@ hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const
       // size the LDS ring identically)
       const int njo = (dmax <= 16 && njw <= 2) ? 1 : 2;
       int ntm = njw <= 2 ? 1 : (njw == 4 ? 2 : 4);
-      constexpr int tpw = DGPRF_TILE_TPW_DEFAULT;
-      bool lean = DGPRF_TILE_LEAN && DGPRF_TILE_G8 && !wide0 && tpw == 1 && njw == 1 && njo == 1;
+      constexpr int tpw = TILE_TPW_DEFAULT;
+      bool lean = !wide0 && tpw == 1 && njw == 1 && njo == 1;
       for (int l = 0; l < pl.n_layers; ++l) lean = lean && pl.n_gp[l] <= 8 && pl.d[l] <= 8;
       if (lean) ntm = 0;
       const TileLds T = tile_lds(pl, ntm, njo, tpw, wide0);

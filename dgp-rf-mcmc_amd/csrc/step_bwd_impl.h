@@ -36,7 +36,7 @@ __device__ __forceinline__ void stage_slice_lds(const LayerK& a, const float* W,
 
 // NWB: waves per workgroup (8: W-only, whole-slice LDS image).
 template <int KS, int NOT, bool RBF, bool G1, bool FB, int NWB>
-__global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT == 1 && !FB && (KS == 1 || KS == 2 || (KS == 4 && !RBF))) ? DGPRF_STEP_WPE : 1))) void k_step_bwd(const LayerK a) {
+__global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT == 1 && !FB && (KS == 1 || KS == 2 || (KS == 4 && !RBF))) ? STEP_WPE : 1))) void k_step_bwd(const LayerK a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr bool WST = NWB == 8;  // whole-slice staging (a.wstage == 1 exactly then)
   int rt, sl;

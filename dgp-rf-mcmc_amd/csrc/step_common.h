@@ -496,21 +496,11 @@ __device__ __forceinline__ void w_update_quad(const K& a, const int e0, const in
     }
     gr = sacc;
   }
-#ifndef DGPRF_UPD_WT
-#define DGPRF_UPD_WT 0
-#endif
-  // theta / momenta / gradient stores (DGPRF_UPD_WT: write-through, the 2 w_total floats of a
-  // large model not left dirty in the L2s at the boundary to the next step's forward)
+  // theta / momenta / gradient stores (write-through stores here gained nothing: 116.1 vs 116.3,
+  // 97.5 vs 97.2 us/step on configs 4 / 5)
   auto store = [&](float* base, f4 v) {  // base: the chain's array (w_total floats)
     float* p = base + e0;
-    if (DGPRF_UPD_WT) {
-      const rsrc_t r = make_rsrc(base, a.w_total);
-      if (nlive == 4) {
-        bstore4_wt(v, r, off);
-      } else {
-        for (int k = 0; k < nlive; ++k) bstore1_wt(v[k], r, off + 4 * k);
-      }
-    } else if (nlive == 4) {
+    if (nlive == 4) {
       *reinterpret_cast<f4*>(p) = v;
     } else {
       for (int k = 0; k < nlive; ++k) p[k] = v[k];
@@ -551,9 +541,7 @@ __device__ __forceinline__ void w_update_quad(const K& a, const int e0, const in
 // chain-steps/s at C = 64 and single-chain 36.3k -> 36.7k steps/s (config 3's ARC layers +3 %);
 // the wider / full-Bayes instances keep their registers (they would spill 20-200 VGPRs; config 5's
 // RBF d = 16 layers lost 8 % with 22 spilled).
-#ifndef DGPRF_STEP_WPE
-#define DGPRF_STEP_WPE 3
-#endif
+constexpr int STEP_WPE = 3;
 
 inline LayerK make_layer_k(const dgprf_plan_t& pl, const StepDev& sd, int l, int& lds_floats,
                     bool bwd = false, int nwb = NW) {

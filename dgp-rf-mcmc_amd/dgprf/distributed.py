@@ -47,8 +47,10 @@ def chain_model(build, model_seed, rank):
 
 
 def gather_accumulators(m, s, e, S_local, group=None):
-    """All-gather per-rank LSE accumulators [C, n] -> [W*C, n] in rank order, and sum S."""
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+    """All-gather per-rank LSE accumulators [C, n] -> [W*C, n] in rank order, and sum S.  Without
+    a process group the local accumulators are the whole; a one-rank group still runs the
+    collective (the code path of the N-GPU runs)."""
+    if not (dist.is_available() and dist.is_initialized()):
         return m, s, e, S_local
     W = dist.get_world_size(group)
     # RCCL ("nccl") gathers device tensors over xGMI; gloo (CPU tests, or several ranks sharing one

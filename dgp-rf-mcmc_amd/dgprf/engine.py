@@ -13,6 +13,7 @@ stream; torch only provides memory, streams and collectives.
 import ctypes
 import math
 
+import numpy as np
 import torch
 
 from . import _native as N
@@ -226,6 +227,39 @@ class Engine:
         pl = self.layout
         c = chain if self.per_chain_hyp else 0
         return self.hyp[c * pl.hyp_total:(c + 1) * pl.hyp_total]
+
+    # ---------------------------------------------------------------- checkpoint / resume
+    _STATE = ("theta", "mom", "mass", "z", "hyp", "hmom", "hmass", "step_ctr")
+
+    def state_arrays(self):
+        """The chain state as host arrays (SURVEY §5 checkpoint / resume): every tensor a step
+        reads or writes — W (theta), momenta, masses, z, hyper-parameters and their momenta /
+        masses, the device step counter (Philox counter, minibatch position, schedule clock) —
+        plus the engine's Philox key and the moment flags.  Omega / c / sigma^2 are derived (rebuilt
+        from z and hyp on load)."""
+        out = {k: getattr(self, k).detach().cpu().numpy() for k in self._STATE}
+        out["seed"] = np.array([self.seed], dtype=np.uint64)
+        out["flags"] = np.array([self.C, int(self.per_chain_hyp), int(self.moments_ready),
+                                 int(self.hyper_moments_ready)], dtype=np.int64)
+        return out
+
+    def load_state_arrays(self, st):
+        """Inverse of state_arrays on an engine of the same spec and chain count."""
+        C, pch, mr, hmr = (int(x) for x in st["flags"])
+        if C != self.C or bool(pch) != self.per_chain_hyp:
+            raise ValueError(f"checkpoint of {C} chains (per_chain_hyp={bool(pch)}) does not match "
+                             f"this engine ({self.C}, {self.per_chain_hyp})")
+        for k in self._STATE:
+            t = getattr(self, k)
+            a = torch.as_tensor(np.asarray(st[k]))
+            if tuple(a.shape) != tuple(t.shape) or a.dtype != t.dtype:
+                raise ValueError(f"checkpoint field {k}: {tuple(a.shape)} {a.dtype}, engine has "
+                                 f"{tuple(t.shape)} {t.dtype}")
+            t.copy_(a.to(t.device))
+        self.seed = int(np.asarray(st["seed"], dtype=np.uint64)[0])
+        self.moments_ready, self.hyper_moments_ready = bool(mr), bool(hmr)
+        self.invalidate_omega()
+        self.build_omega()
 
     # ---------------------------------------------------------------- per-B plans
     def plan_ws(self, B, fresh_z=0, full_bayes=False):
@@ -531,10 +565,18 @@ class Engine:
         omega [d, R] -> A [n, R]."""
         X = as_device(X, self.dev)
         omega = as_device(omega, self.dev)
+        if X.dim() != 2 or omega.dim() != 2:
+            raise ValueError("rf_project: X [n, ldx] and omega [d, R] must be 2-D")
         n, ldx = X.shape
         d, R = omega.shape
+        if ldx < d:
+            raise ValueError(f"rf_project: X has {ldx} columns, omega needs {d}")
         if out is None:
             out = torch.empty(n, R, dtype=_F32, device=self.dev)
+        elif (tuple(out.shape) != (n, R) or out.dtype != _F32 or not out.is_contiguous()
+              or out.device != X.device):
+            raise ValueError(f"rf_project: out must be a contiguous fp32 [{n}, {R}] tensor on "
+                             f"{X.device}, got {tuple(out.shape)} {out.dtype} on {out.device}")
         N.call("dgprf_rf_project", ptr(X), int(n), int(ldx), int(d), ptr(omega), int(R), ptr(out),
                stream())
         return out

@@ -176,7 +176,9 @@ class DGP_RF(Module):
         eng = self._engine
         fresh = [l for l in range(self.n_hidden_layers) if not self.BNN.layers[2 * l].random_fixed]
         if not fresh:
-            eng.build_omega()
+            # fixed z: Omega / c / sigma^2 only when z or a hyper-parameter changed since the last
+            # build (engine version keys), as the graph path does
+            eng.build_omega_if_stale()
             return None
         z = eng.z.clone()
         for l in fresh:
@@ -193,7 +195,7 @@ class DGP_RF(Module):
         eng = self._engine
         fresh = [l for l in range(self.n_hidden_layers) if not self.BNN.layers[2 * l].random_fixed]
         if not fresh:
-            eng.build_omega()
+            eng.build_omega_if_stale()
             return None, None
         z = eng.z.clone()
         for l in fresh:
@@ -390,6 +392,21 @@ class DGP_RF(Module):
         """{'W_l': copy of GP layer l's W} — the helper experiments/utils_training_demo.py:57,140
         calls (absent from the reference's models/)."""
         return {'W_' + str(i): W.detach().clone() for i, W in enumerate(self.W_mcmc)}
+
+    def save(self, path):
+        """Checkpoint the sampler: an .npz of every W, the momenta and masses, z, the
+        kernel / likelihood hyper-parameters with their momenta and masses, the device step counter
+        and the Philox key — the state the reference keeps only as live tf.Variable aliases
+        (experiments/utils_training.py:226,306).  Resuming from it continues the chain bit-exactly."""
+        np.savez(path, **self._engine.state_arrays())
+
+    def load(self, path):
+        """Restore a checkpoint written by save() into a model of the same construction."""
+        with np.load(path, allow_pickle=False) as st:
+            self._engine.load_state_arrays({k: st[k] for k in st.files})
+        eng = self._engine
+        if eng.moments_ready:
+            self._attach_sampler_attrs(full_bayesian=eng.hyper_moments_ready)
 
     def set_random_fixed(self, state):
         for l in range(self.n_hidden_layers):

@@ -337,7 +337,8 @@ int dgprf_gp_matmul(const float *phi, int64_t n, int32_t P, const float *W, int3
 /* The RF projection of one layer, A = X Omega (RBFLayer / ARCLayer `tf.matmul(x, self.Omega)`,
  * layers/rf_layers.py:42, 88): A[n][R] = X[n][0:d] Omega[d][R], X with row stride ldx >= d, as the
  * hand-written fp32 MFMA GEMM the wide first layer of the step and of the predictive forward runs
- * (32 x 128 tiles up to 1,024 rows, 128 x 128 beyond).  d, ldx and R multiples of 4 for the MFMA
+ * (64 x 64 tiles with K whole up to 1,024 rows, 128 x 128 beyond; the step's own A_1 GEMM runs
+ * 64 x 64 tiles in two K parts).  d, ldx and R multiples of 4 for the MFMA
  * kernel (other shapes take the LDS-tiled 16x16x4 fallback).  ABI 7. */
 int dgprf_rf_project(const float *X, int64_t n, int32_t ldx, int32_t d, const float *omega,
                      int32_t R, float *A, void *stream);

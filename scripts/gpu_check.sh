@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round-4 GPU check: the GPU test suite, then (only if it is green) a bench run.
-#   TAG=... PYTEST_ARGS="-k ..." BENCH_ARGS="..." scripts/gpu_check_r04.sh
+# GPU check: the GPU test suite, then (only if it is green) a bench run.
+#   TAG=... PYTEST_ARGS="-k ..." BENCH_ARGS="..." scripts/gpu_check.sh
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 O=gpurun_out/${TAG:-r4}
 mkdir -p $O

@@ -4,7 +4,7 @@
 # traces of the config 4 / 5 steps.  Each step has its own time limit; the first failure ends it.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 R=$PWD
-TAG=${TAG:-r04}
+TAG=${TAG:-r05}
 O=$R/gpurun_out/final_$TAG
 P=$R/profiles/$TAG
 mkdir -p $O $P

@@ -7,7 +7,7 @@
 # Everything is also written under gpurun_out/prof_$TAG (the only part that comes back).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 R=$PWD
-TAG=${TAG:-r04}
+TAG=${TAG:-r05}
 O=$R/gpurun_out/prof_$TAG
 P=$R/profiles/$TAG
 mkdir -p $O $P

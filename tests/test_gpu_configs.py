@@ -268,6 +268,51 @@ def test_wide_first_layer_full_bayes_grad(dev):
     assert group_err([h[0], h[1]], [ref["log_amp"][0], ref["log_amp"][1]]) < 5e-4
 
 
+def test_wide_first_layer_two_chains_two_k_parts(dev):
+    """C = 2 chains with a wide first layer (d = 100 > 32) at B = 96: the step's A_1 GEMM in two K
+    parts (agemm.hip: blockIdx.y = chain x 2 + part, per-chain slab strides) feeding the layer-0
+    forward / backward, which add slab 0 + slab 1 — each chain's gradient against the oracle with
+    that chain's W, and chain 0 of 2-chain graph steps bitwise equal to a 1-chain engine."""
+    from dgprf import engine as E
+    from likelihoods import Softmax
+    from models.dgp import DGP_RF
+    E.set_seed(53)
+    kinds, n_rf, n_gp = ["RBF", "RBF"], [256, 128], [10, 5]
+    m = DGP_RF(100, 5, n_hidden_layers=2, n_rf=n_rf, n_gp=n_gp, likelihood=Softmax(),
+               kernel_type_list=kinds)
+    one = m._engine
+    two = E.Engine(one.spec, 2, seed=one.seed)
+    two.z.copy_(one.z)
+    two.hyp.copy_(one.hyp)
+    two.theta[0].copy_(one.theta[0])
+    E.normal(None, 4, out=two.theta[1])
+    assert two.layout.a0_off >= 0
+    rng = np.random.default_rng(10)
+    X = rng.uniform(-1, 1, (96, 100)).astype(np.float32).astype(np.float64)
+    Y = rng.integers(0, 5, (96, 1)).astype(float)
+    two.build_omega()
+    G = two.grad(X, Y, 5000)
+    for c in range(2):
+        W = [cpu(two.theta[c, two.layout.w_off[l]:two.layout.w_off[l] + two.layout.P[l] * n_gp[l]])
+             .reshape(two.layout.P[l], n_gp[l]) for l in range(2)]
+        p = O.Params(100, 5, n_rf, n_gp, kinds, "softmax", False,
+                     z=[cpu(m.BNN.layers[2 * l].z) for l in range(2)], W=W,
+                     log_inv_ls=[cpu(k.log_inv_length_scale) for k in m.kernel_list])
+        ref = O.grad_W(p, X, Y, 5000)
+        got = unpack(two, G, chain=c)
+        for l in range(2):
+            assert rel_err(got[l], ref[l]) < 2e-4, (c, l)
+    n = 960
+    Xd = torch.rand(n, 100, device=dev) * 2 - 1
+    Yd = torch.randint(0, 5, (n, 1), device=dev).float()
+    for e in (one, two):
+        e.mom.zero_()
+        e.build_omega()
+        e.graph(Xd, Yd, 96, n, 0.02, 0.9, 1.0, 5).launch()
+    assert torch.equal(one.theta[0], two.theta[0])
+    assert torch.isfinite(two.theta).all() and not torch.equal(two.theta[0], two.theta[1])
+
+
 @pytest.mark.parametrize("n,d,ldx,R", [(200, 784, 784, 4096), (1024, 784, 784, 4096),
                                        (1025, 784, 784, 4096), (10_000, 784, 784, 4096),
                                        (77, 30, 33, 500), (1500, 36, 40, 1000)])

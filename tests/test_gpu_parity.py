@@ -335,6 +335,78 @@ def test_graph_replay_equals_eager_steps(dev):
     assert torch.equal(a._engine.mom, b._engine.mom)
 
 
+def test_per_call_sgmcmc_update_equals_graph_replays(dev):
+    """The reference's driver loop — one model.sgmcmc_update(x, y, N, ...) call per minibatch
+    (experiments/utils_training.py:45-61 -> models/dgp.py:184-216) — is bit-equal over 10 steps to
+    run_sgmcmc's graph replays fed the same minibatch rows (the device epoch permutation, restated
+    by the oracle), and builds Omega once (fixed z: only when z or a hyper-parameter is stale)."""
+    from likelihoods import Gaussian
+    from models.regression_model import RegressionDGP
+    from dgprf import engine as E
+    E.set_seed(21)
+    a = RegressionDGP(8, 1, n_hidden_layers=3, n_rf=64, n_gp=[8, 8, 1], likelihood=Gaussian())
+    E.set_seed(21)
+    b = RegressionDGP(8, 1, n_hidden_layers=3, n_rf=64, n_gp=[8, 8, 1], likelihood=Gaussian())
+    n, B, steps = 2000, 200, 10
+    X = torch.randn(n, 8, device=dev)
+    Y = torch.randn(n, 1, device=dev)
+    for mm in (a, b):
+        mm.precond_update(None, n, precond_type="identity")
+    b._engine.mom.copy_(a._engine.mom)
+    a.run_sgmcmc(X, Y, n, steps, batch_size=B, lr=0.01, momentum_decay=0.9, steps_per_graph=steps,
+                 perm_seed=5)
+    eng = b._engine
+    calls = []
+    orig = eng.build_omega
+    eng.build_omega = lambda *args, **kw: (calls.append(1), orig(*args, **kw))[1]
+    for t in range(steps):
+        rows = torch.as_tensor(R.batch_rows(t, B, n, n // B, perm_seed=5), device=dev)
+        b.sgmcmc_update(X[rows], Y[rows], n, lr=0.01, momentum_decay=0.9)
+    assert len(calls) <= 1  # Omega built at most once over the 10 calls
+    assert int(a._engine.step_ctr) == steps == int(eng.step_ctr)
+    assert torch.equal(a._engine.theta, eng.theta)
+    assert torch.equal(a._engine.mom, eng.mom)
+    with torch.no_grad():  # a hyper-parameter write makes the next call rebuild
+        b.kernel_list[1].log_inv_length_scale.sub_(0.05)
+    n0 = len(calls)
+    b.sgmcmc_update(X[:B], Y[:B], n, lr=0.01, momentum_decay=0.9)
+    assert len(calls) == n0 + 1
+
+
+def test_checkpoint_resume_bit_exact(dev, tmp_path):
+    """save() at step 100 -> load() into a freshly built model -> 100 more graph-replayed steps is
+    bitwise the 200 uninterrupted steps (SURVEY §5 checkpoint / resume; the reference keeps only
+    live variable aliases, experiments/utils_training.py:226)."""
+    from likelihoods import Gaussian
+    from models.regression_model import RegressionDGP
+    from dgprf import engine as E
+    mk = lambda: RegressionDGP(8, 1, n_hidden_layers=3, n_rf=64, n_gp=[8, 8, 1],
+                               likelihood=Gaussian())
+    E.set_seed(31)
+    a = mk()
+    n = 3000
+    X = torch.randn(n, 8, device=dev)
+    Y = torch.randn(n, 1, device=dev)
+    a.precond_update(None, n, precond_type="identity")
+    run = dict(batch_size=200, lr=0.01, momentum_decay=0.9, steps_per_graph=50, perm_seed=4)
+    a.run_sgmcmc(X, Y, n, 100, **run)
+    path = str(tmp_path / "ckpt.npz")
+    a.save(path)
+    a.run_sgmcmc(X, Y, n, 100, **run)
+    E.set_seed(999)  # a different construction draw: everything must come from the checkpoint
+    b = mk()
+    b.load(path)
+    assert int(b._engine.step_ctr) == 100 and b._engine.seed == a._engine.seed
+    assert b.W_mcmc[0].moments is not None
+    b.run_sgmcmc(X, Y, n, 100, **run)
+    torch.cuda.synchronize()
+    for t in ("theta", "mom", "mass", "hyp", "z", "step_ctr"):
+        assert torch.equal(getattr(a._engine, t), getattr(b._engine, t)), t
+    with pytest.raises(ValueError):  # a checkpoint of another shape is refused
+        RegressionDGP(8, 1, n_hidden_layers=3, n_rf=32, n_gp=[8, 8, 1],
+                      likelihood=Gaussian()).load(path)
+
+
 def test_sgmcmc_graphs_rebuild_omega_only_when_stale(dev):
     """sgmcmc_graphs builds Omega / c / sigma^2 only when z or a hyper-parameter changed since the
     last build (torch version counters of the packed buffers): a second call with nothing changed

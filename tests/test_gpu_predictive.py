@@ -164,12 +164,13 @@ def _free_port():
     return p
 
 
-def _rank_worker(rank, world, port, q):
+def _rank_worker(rank, world, port, q, backend="gloo"):
     """One rank: 2 chains of its own (rank-keyed draws of W) over the shared test set and model,
     2 samples each; PredictiveLSE.finalize all-gathers the accumulators (gloo: host-staged, two
-    ranks share the one GPU) and runs k_lse_finalize on the stacked [world * 2, n] rows.  The
-    model comes from the helper bench.py uses (dgprf.distributed.chain_model): z and the
-    hyper-parameters are gathered and must be bitwise equal on every rank (one posterior)."""
+    ranks share the one GPU; nccl = RCCL: device tensors, one rank per GPU) and runs
+    k_lse_finalize on the stacked [world * 2, n] rows.  The model comes from the helper bench.py
+    uses (dgprf.distributed.chain_model): z and the hyper-parameters are gathered and must be
+    bitwise equal on every rank (one posterior)."""
     from dgprf import _native as N
     from dgprf import engine as E
     from dgprf.data import regression_data
@@ -177,14 +178,19 @@ def _rank_worker(rank, world, port, q):
     from dgprf.predictive import PredictiveLSE
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world,
+                                device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    xfer = (lambda t: t) if backend == "nccl" else (lambda t: t.cpu())
     Xt, Yt, _ = regression_data(5_003, CFG2["D"], seed=6, device="cuda")
     m = chain_model(_build_config2, 8, rank)
     eng = m._engine
     eng.build_omega()
     for t in (eng.z, eng.hyp, eng.omega):  # one model on every rank
-        parts = [torch.empty_like(t.cpu()) for _ in range(world)]
-        dist.all_gather(parts, t.cpu())
+        parts = [torch.empty_like(xfer(t)) for _ in range(world)]
+        dist.all_gather(parts, xfer(t))
         assert all(torch.equal(parts[0], p) for p in parts), "ranks built different models"
     seeds = [None] * world
     dist.all_gather_object(seeds, (eng.seed, float(eng.theta[0, 0])))
@@ -203,13 +209,16 @@ def _rank_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_predictive_two_ranks_gather_and_finalize(dev):
-    """world_size 2 through PredictiveLSE.finalize (gather_accumulators + k_lse_finalize) on the
-    GPU: both ranks report the same LL / RMSE, equal to the oracle over all 8 samples."""
-    world, port = 2, _free_port()
+@pytest.mark.parametrize("world,backend", [(2, "gloo"), (1, "nccl")])
+def test_predictive_two_ranks_gather_and_finalize(dev, world, backend):
+    """PredictiveLSE.finalize (gather_accumulators + k_lse_finalize) on the GPU: world_size 2 over
+    gloo (both ranks on the one GPU), and a one-rank nccl (= RCCL) group, whose all-gather runs the
+    device-tensor branch the 8-GPU runs take (dgprf/distributed.py); every rank reports the same
+    LL / RMSE, equal to the oracle over all world x 2 x 2 samples."""
+    port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = mp.spawn(_rank_worker, args=(world, port, q), nprocs=world, join=False)
+    procs = mp.spawn(_rank_worker, args=(world, port, q, backend), nprocs=world, join=False)
     # drain the queue before joining: a child cannot exit while its queued arrays sit in the pipe
     res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda r: r[0])
     procs.join()
@@ -228,4 +237,4 @@ def test_predictive_two_ranks_gather_and_finalize(dev):
     ref_ll, ref_rmse = O.predictive_summary(np.stack(lp_all), np.stack(se_all), y_std=1.3)
     for _, _, ll, rmse in res:
         assert abs(ll - ref_ll) < 1e-4 and abs(rmse - ref_rmse) < 1e-5 * ref_rmse
-    assert res[0][2] == res[1][2] and res[0][3] == res[1][3]
+    assert all(r[2] == res[0][2] and r[3] == res[0][3] for r in res)
