@@ -515,13 +515,10 @@ def main():
     # Per-kernel device time: the event pair around each kernel minus an empty pair recorded the
     # same way (the pair's own cost); the steady-state step time itself comes from the events over
     # the timed region (step_ms_dev), whose remainder is kernel-boundary time.
-    # plan.ipu: the update is folded into the backward launches (no update kernel)
-    folded = bool(eng.plan_ws(B)[0].ipu)
-    inflow = list(prof["fwd"]) + list(prof["bwd"]) + ([] if folded else [prof["update"]])
+    inflow = list(prof["fwd"]) + list(prof["bwd"]) + [prof["update"]]
     att = [max(x - prof["empty"], 1e-6) for x in inflow]
     Lk = len(prof["fwd"])
-    att_fwd, att_bwd = att[:Lk], att[Lk:2 * Lk]
-    att_upd = None if folded else att[2 * Lk]
+    att_fwd, att_bwd, att_upd = att[:Lk], att[Lk:2 * Lk], att[2 * Lk]
     per_name = {
         "k_step_fwd": (sum(att_fwd) / Lk, sum(fwd_f) / Lk, Lk),
         "k_step_bwd": (sum(att_bwd) / Lk, sum(bwd_f) / Lk, Lk),
@@ -540,7 +537,7 @@ def main():
     # launch stream minus an empty pair) is reported beside it and must agree within 15 %
     # (tests/test_bench_profiles.py).  Without a committed trace the live span is used.
     use_us = rp_us if rp_us else live_us
-    n_launch = 2 * len(d) + (0 if folded else 1)
+    n_launch = 2 * len(d) + 1
     bnd_us = launch_boundary_us(dev)
     rel = os.path.relpath(PROFILES, ROOT)
     roof = {"kernel": dom, "bound": "mfma",
@@ -581,13 +578,9 @@ def main():
             "empty_pair_us": round(prof["empty"] * 1e3, 3),
             "step_kernel_us": {"fwd": [round(x * 1e3, 3) for x in att_fwd],
                                "bwd": [round(x * 1e3, 3) for x in att_bwd],
-                               "update": None if folded else round(att_upd * 1e3, 3)},
-            "update_folded": folded,
-            "update_form": ("folded into the backward: the last of each feature slice's row-tile "
-                            "workgroups sums the slice's gW partial rows and updates it in place "
-                            "(plan.ipu)" if folded else "separate update kernel"),
+                               "update": round(att_upd * 1e3, 3)},
             "inflow_event_us": [round(x * 1e3, 3) for x in inflow],
-            "update_hbm_GBps": None if folded else round(upd_bytes / (att_upd * 1e-3) / 1e9, 2),
+            "update_hbm_GBps": round(upd_bytes / (att_upd * 1e-3) / 1e9, 2),
             "regime": "latency-bound at B=200: 51.6 MFLOP/step; see DESIGN.md"}
     fp = pred_flops(CFG["N_test"], d, R, P, g)
     n_trans = CFG["N_test"] * sum(2 * r for r in R)  # sin + cos per RBF feature per test row

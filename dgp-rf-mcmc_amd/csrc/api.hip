@@ -3,7 +3,6 @@
 // Host-side validation and planning mirror the reference's constructor and assertions
 // (models/dgp.py:34-52, 74-115; kernels/RBF.py:19-27; kernels/arc_cosine.py:13-16): configuration
 // errors are reported as return codes before anything is enqueued.
-#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -49,13 +48,6 @@ StepDev make_step_dev(const dgprf_plan_t& pl, const dgprf_chain_t& ch, const dgp
   sd.hyp = ch.hyp;
   sd.hmom = ch.hmom;
   sd.hmass = ch.hmass;
-  sd.xb = ch.ws ? ch.ws + pl.xb_off : nullptr;
-  sd.yb = ch.ws ? ch.ws + pl.yb_off : nullptr;
-  sd.xb_next = ch.ws ? ch.ws + pl.xb2_off : nullptr;
-  sd.yb_next = ch.ws ? ch.ws + pl.yb2_off : nullptr;
-  sd.gather_next = 0;
-  sd.ipu = 0;
-  std::memset(&sd.ud, 0, sizeof(sd.ud));
   return sd;
 }
 
@@ -114,44 +106,24 @@ int check_step(const dgprf_step_t* st) {
   return DGPRF_OK;
 }
 
-// Whether a step folds its update into the backward (plan.ipu): W-only SGHMC steps (not
-// gradient-only, not full-Bayes).
-bool step_ipu(const dgprf_plan_t& pl, const StepDev& sd, const UpdateDev& ud) {
-  return pl.ipu && !ud.grad_only && !sd.full_bayes && sd.ws;
-}
-
 // [gather rows] fwd for every layer, bwd in reverse, then the update.  prep_gather: gather this
-// step's minibatch rows first; gather_next: step t+1's rows are gathered during this step (graph
-// replays, where the next step is known to follow) — by extra workgroups of the layer-0 forward
-// into the other gathered-rows buffer (step k of a graph reads buffer k % 2), or, after the
-// all-layer fused forward, by the update kernel.  The update kernel sums the gW partials and
-// updates every W (and the full-Bayes hyper-parameters); with plan.ipu the backward does that for
-// W-only steps and there is no update launch.
-hipError_t enqueue_step(const dgprf_plan_t& pl, const StepDev& sd_in, const UpdateDev& ud,
-                        hipStream_t s, bool prep_gather = true, bool gather_next = false,
-                        int k = 0) {
+// step's minibatch rows first; gather_next: the update kernel gathers step t+1's rows (graph
+// replays, where the next step is known to follow).  The update kernel sums the gW partials and
+// updates every W (and the full-Bayes hyper-parameters).
+hipError_t enqueue_step(const dgprf_plan_t& pl, const StepDev& sd, const UpdateDev& ud,
+                        hipStream_t s, bool prep_gather = true, bool gather_next = false) {
   hipError_t e = hipSuccess;
-  StepDev sd = sd_in;
-  if (sd.ws && (k & 1)) {  // odd steps of a graph read the second buffer
-    std::swap(sd.xb, sd.xb_next);
-    std::swap(sd.yb, sd.yb_next);
-  }
-  const bool fused = dgprf_sk::step_fused_fwd(pl);
-  sd.gather_next = gather_next && !fused;
-  sd.ipu = step_ipu(pl, sd, ud);
-  sd.ud = ud;
   if (prep_gather) e = dgprf::launch_gather(pl, sd, s);
   // random_fixed=False layers: this step's Omega from fresh z (layers/rf_layers.py:39-41)
   if (e == hipSuccess && pl.fresh_z) e = dgprf::launch_fresh_omega(pl, sd, s);
-  if (fused) {  // large B, one chain: one all-layer forward launch
+  if (dgprf_sk::step_fused_fwd(pl)) {  // large B, one chain: one all-layer forward launch
     if (e == hipSuccess) e = dgprf::launch_step_fwd_fused(pl, sd, s);
   } else {
     for (int l = 0; l < pl.n_layers && e == hipSuccess; ++l) e = dgprf::launch_step_fwd(pl, sd, l, s);
   }
   for (int l = pl.n_layers - 1; l >= 0 && e == hipSuccess; --l)
     e = dgprf::launch_step_bwd(pl, sd, l, s);
-  if (e == hipSuccess && !sd.ipu)
-    e = dgprf::launch_step_update(pl, sd, ud, nullptr, s, gather_next && fused);
+  if (e == hipSuccess) e = dgprf::launch_step_update(pl, sd, ud, nullptr, s, gather_next);
   return e;
 }
 
@@ -194,8 +166,7 @@ int dgprf_plan_init(dgprf_plan_t* pl) {
   if (pl->d_in < 1 || pl->d_out < 1 || pl->batch < 1 || pl->n_chains < 1) return DGPRF_E_SHAPE;
   if (pl->likelihood != DGPRF_LIK_GAUSSIAN && pl->likelihood != DGPRF_LIK_SOFTMAX) return DGPRF_E_ARG;
   if (pl->fwd_path < DGPRF_FWD_AUTO || pl->fwd_path > DGPRF_FWD_ROWS8 || pl->agemm_chunk_rows < 0 ||
-      pl->fresh_z < 0 || (pl->fresh_z >> L) != 0 || (pl->bwd_tiles != 0 && pl->bwd_tiles != 1) ||
-      (pl->sep_update != 0 && pl->sep_update != 1))
+      pl->fresh_z < 0 || (pl->fresh_z >> L) != 0 || (pl->bwd_tiles != 0 && pl->bwd_tiles != 1))
     return DGPRF_E_ARG;
   for (int l = 0; l < L; ++l) {
     if (pl->kind[l] != DGPRF_RBF && pl->kind[l] != DGPRF_ARC) return DGPRF_E_ARG;
@@ -267,7 +238,7 @@ int dgprf_plan_init(dgprf_plan_t* pl) {
   // keeps its gW in accumulators (k_step_bwd_rg), so the gW partials stay <= 16 rows
   pl->rt_per_group = 1;
   pl->rg_full_bayes = 0;
-  pl->pad1 = pl->pad2 = 0;
+  pl->pad1 = 0;
   if (pl->n_row_tiles > 16 && !pl->bwd_tiles) {
     bool ok = true, ok_fb = true;
     dgprf_sk::RgCfg c;
@@ -301,15 +272,6 @@ int dgprf_plan_init(dgprf_plan_t* pl) {
   ws = align4(ws + (int64_t)B * pl->d_in);
   pl->yb_off = ws;
   ws = align4(ws + (int64_t)B * pl->yb_cols);
-  // the other buffer of the double-buffered gathered rows (a graph's step k reads buffer k % 2
-  // while step k's first kernel gathers step k + 1's rows into the other)
-  pl->xb2_off = ws;
-  ws = align4(ws + (int64_t)B * pl->d_in);
-  pl->yb2_off = ws;
-  ws = align4(ws + (int64_t)B * pl->yb_cols);
-  // arrival counters of the folded update, one per (layer, feature slice)
-  pl->cnt_off = ws;
-  ws = align4(ws + (int64_t)DGPRF_MAX_LAYERS * DGPRF_NS_MAX);
   pl->omf_off = -1;
   if (pl->fresh_z) {
     pl->omf_off = ws;
@@ -325,14 +287,6 @@ int dgprf_plan_init(dgprf_plan_t* pl) {
   // the row-group / row-wave backward kernels address a chain's workspace with 32-bit buffer
   // offsets: refuse the plan here rather than failing every step at launch
   if (pl->rt_per_group > 1 && ws >= ((int64_t)1 << 29)) return DGPRF_E_SHAPE;
-  // folded update (W-only steps): per-row-tile backward, small slices, 32-bit workspace offsets
-  bool ipu = pl->rt_per_group == 1 && pl->n_row_tiles <= 16 && !pl->sep_update &&
-             ws < ((int64_t)1 << 29);
-  for (int l = 0; l < L && ipu; ++l) {
-    const int64_t nf = std::min<int64_t>(64 * (int64_t)pl->cpw[l], pl->n_rf[l]);
-    ipu = nf * (pl->kind[l] == DGPRF_RBF ? 2 : 1) * pl->n_gp[l] <= DGPRF_IPU_MAX_SLICE;
-  }
-  pl->ipu = ipu ? 1 : 0;
   pl->ws_chain = ws;
   pl->ws_total = ws * pl->n_chains;
   pl->initialised = 1;
@@ -416,7 +370,7 @@ int dgprf_graph_create_sghmc(dgprf_graph_handle* out, const dgprf_plan_t* plan,
   for (int k = 0; k < steps_per_graph && e == hipSuccess; ++k) {
     StepDev sd = make_step_dev(*plan, *chain, *batch, st.step_offset + k);
     sd.full_bayes = st.full_bayes != 0;
-    e = enqueue_step(*plan, sd, ud, cs, k == 0, k + 1 < steps_per_graph, k);
+    e = enqueue_step(*plan, sd, ud, cs, k == 0, k + 1 < steps_per_graph);
   }
   if (e == hipSuccess) e = dgprf::launch_advance(chain->step, steps_per_graph, cs);
   hipGraph_t g = nullptr;
@@ -476,13 +430,10 @@ int dgprf_profile_step(const dgprf_plan_t* plan, const dgprf_chain_t* chain,
   for (int k = 0; k <= K + 1; ++k) ms_out[k] = 0.f;
   // the real step sequence (fwd 0..L-1, bwd L-1..0, update), every kernel between two events
   for (int rep = 0; rep < reps && e == hipSuccess; ++rep) {
-    StepDev sd = make_step_dev(*plan, *chain, *batch, st.step_offset);
-    sd.ud = ud;
-    sd.ipu = step_ipu(*plan, sd, ud);  // folded update: no update launch (its slot reads 0)
+    const StepDev sd = make_step_dev(*plan, *chain, *batch, st.step_offset);
     e = dgprf::launch_gather(*plan, sd, s);
     for (int j = 0; j < K && e == hipSuccess; ++j) {
       const int kk = j < L ? j : (j < 2 * L ? L + (2 * L - 1 - j) : 2 * L);
-      if (kk == 2 * L && sd.ipu) continue;
       if (kk == 0 && ag) {
         e = hipEventRecord(ev[2 * (K + 1)], s);
         if (e == hipSuccess) e = dgprf::launch_step_agemm(*plan, sd, s);
@@ -502,7 +453,6 @@ int dgprf_profile_step(const dgprf_plan_t* plan, const dgprf_chain_t* chain,
     if (e == hipSuccess) e = hipEventRecord(ev[2 * K + 1], s);
     if (e == hipSuccess) e = hipEventSynchronize(ev[2 * K + 1]);
     for (int kk = 0; kk <= K + (ag ? 1 : 0) && e == hipSuccess; ++kk) {
-      if (kk == 2 * L && sd.ipu) continue;
       float ms = 0.f;
       e = hipEventElapsedTime(&ms, ev[2 * kk], ev[2 * kk + 1]);
       ms_out[kk] += ms / (float)reps;

@@ -4,16 +4,6 @@
 
 #include "dgprf_device.h"
 
-struct UpdateDev {
-  float lr, beta, temperature, data_size;
-  int32_t resample, schedule, grad_only, resample_head;
-  int64_t start_step, cycle_length;
-  const float* xi;
-  const float* xi_resample;
-  const float* xi_hyp;
-  const float* xi_hyp_resample;
-};
-
 // Everything a step kernel needs besides the plan (passed by value as a kernel argument).
 struct StepDev {
   float* theta;
@@ -35,15 +25,16 @@ struct StepDev {
   float* hyp;
   float* hmom;
   const float* hmass;
-  // gathered minibatch rows this step reads (one of the plan's two buffers, chain 0) and the
-  // buffer the next step's rows are gathered into (gather_next)
-  float* xb;
-  float* yb;
-  float* xb_next;
-  float* yb_next;
-  int32_t gather_next;  // step t+1's rows are gathered by this step (graph replays)
-  int32_t ipu;          // the backward folds the SGHMC update (plan.ipu, W-only step): no update launch
-  UpdateDev ud;         // the update the folded backward applies (ipu)
+};
+
+struct UpdateDev {
+  float lr, beta, temperature, data_size;
+  int32_t resample, schedule, grad_only, resample_head;
+  int64_t start_step, cycle_length;
+  const float* xi;
+  const float* xi_resample;
+  const float* xi_hyp;
+  const float* xi_hyp_resample;
 };
 
 // In-kernel timestamps for a separate diagnostic build (-DDGPRF_STAMPS); never in the product.

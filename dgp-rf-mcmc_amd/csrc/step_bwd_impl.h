@@ -34,9 +34,8 @@ __device__ __forceinline__ void stage_slice_lds(const LayerK& a, const float* W,
 }
 
 
-// NWB: waves per workgroup (8: W-only, whole-slice LDS image).  IPU: fold the SGHMC update of
-// the slice into this launch (ipu_slice, W-only steps with plan.ipu).
-template <int KS, int NOT, bool RBF, bool G1, bool FB, int NWB, bool IPU>
+// NWB: waves per workgroup (8: W-only, whole-slice LDS image).
+template <int KS, int NOT, bool RBF, bool G1, bool FB, int NWB>
 __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT == 1 && !FB && (KS == 1 || KS == 2 || (KS == 4 && !RBF))) ? STEP_WPE : 1))) void k_step_bwd(const LayerK a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr bool WST = NWB == 8;  // whole-slice staging (a.wstage == 1 exactly then)
@@ -472,7 +471,6 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
       }
     }
   }
-  if constexpr (IPU) ipu_slice<RBF>(a, chain, sl, reinterpret_cast<int*>(red));
 #ifdef DGPRF_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
@@ -480,46 +478,39 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
 }
 
 // backward: KS x NOT x RBF x G1 x FB x waves per workgroup (8: W-only with whole-slice staging)
-// x IPU (W-only)
 template <int KS, int NOT, bool G1>
-void k_step_bwd_launch3(bool rbf, bool fb, bool w8, bool ipu, dim3 grid, size_t lds,
-                        hipStream_t s, const LayerK& a) {
-#define DGPRF_BWD(R_, F_, W_, I_)                                                                \
-  do {                                                                                          \
-    dgprf::set_lds_limit((const void*)k_step_bwd<KS, NOT, R_, G1, F_, W_, I_>, lds);           \
-    hipLaunchKernelGGL((k_step_bwd<KS, NOT, R_, G1, F_, W_, I_>), grid, dim3(64 * W_), lds, s, a); \
+void k_step_bwd_launch3(bool rbf, bool fb, bool w8, dim3 grid, size_t lds, hipStream_t s,
+                        const LayerK& a) {
+#define DGPRF_BWD(R_, F_, W_)                                                                 \
+  do {                                                                                       \
+    dgprf::set_lds_limit((const void*)k_step_bwd<KS, NOT, R_, G1, F_, W_>, lds);            \
+    hipLaunchKernelGGL((k_step_bwd<KS, NOT, R_, G1, F_, W_>), grid, dim3(64 * W_), lds, s, a); \
   } while (0)
   if (rbf) {
-    if (fb) DGPRF_BWD(true, true, 4, false);
-    else if (w8) {
-      if (ipu) DGPRF_BWD(true, false, 8, true);
-      else DGPRF_BWD(true, false, 8, false);
-    } else if (ipu) DGPRF_BWD(true, false, 4, true);
-    else DGPRF_BWD(true, false, 4, false);
+    if (fb) DGPRF_BWD(true, true, 4);
+    else if (w8) DGPRF_BWD(true, false, 8);
+    else DGPRF_BWD(true, false, 4);
   } else {
-    if (fb) DGPRF_BWD(false, true, 4, false);
-    else if (w8) {
-      if (ipu) DGPRF_BWD(false, false, 8, true);
-      else DGPRF_BWD(false, false, 8, false);
-    } else if (ipu) DGPRF_BWD(false, false, 4, true);
-    else DGPRF_BWD(false, false, 4, false);
+    if (fb) DGPRF_BWD(false, true, 4);
+    else if (w8) DGPRF_BWD(false, false, 8);
+    else DGPRF_BWD(false, false, 4);
   }
 #undef DGPRF_BWD
 }
 template <int KS>
-void k_step_bwd_launch2(int g, bool rbf, bool fb, bool w8, bool ipu, dim3 grid, size_t lds,
-                        hipStream_t s, const LayerK& a) {
+void k_step_bwd_launch2(int g, bool rbf, bool fb, bool w8, dim3 grid, size_t lds, hipStream_t s,
+                        const LayerK& a) {
   const int NOT = (g + 15) >> 4;
-  if (g == 1) k_step_bwd_launch3<KS, 1, true>(rbf, fb, w8, ipu, grid, lds, s, a);
-  else if (NOT == 1) k_step_bwd_launch3<KS, 1, false>(rbf, fb, w8, ipu, grid, lds, s, a);
-  else if (NOT == 2) k_step_bwd_launch3<KS, 2, false>(rbf, fb, w8, ipu, grid, lds, s, a);
-  else if (NOT == 3) k_step_bwd_launch3<KS, 3, false>(rbf, fb, w8, ipu, grid, lds, s, a);
-  else k_step_bwd_launch3<KS, 4, false>(rbf, fb, w8, ipu, grid, lds, s, a);
+  if (g == 1) k_step_bwd_launch3<KS, 1, true>(rbf, fb, w8, grid, lds, s, a);
+  else if (NOT == 1) k_step_bwd_launch3<KS, 1, false>(rbf, fb, w8, grid, lds, s, a);
+  else if (NOT == 2) k_step_bwd_launch3<KS, 2, false>(rbf, fb, w8, grid, lds, s, a);
+  else if (NOT == 3) k_step_bwd_launch3<KS, 3, false>(rbf, fb, w8, grid, lds, s, a);
+  else k_step_bwd_launch3<KS, 4, false>(rbf, fb, w8, grid, lds, s, a);
 }
 
 }  // namespace dgprf_sk
 
 #ifdef DGPRF_KS
-template void dgprf_sk::k_step_bwd_launch2<DGPRF_KS>(int, bool, bool, bool, bool, dim3, size_t,
+template void dgprf_sk::k_step_bwd_launch2<DGPRF_KS>(int, bool, bool, bool, dim3, size_t,
                                                        hipStream_t, const dgprf_sk::LayerK&);
 #endif

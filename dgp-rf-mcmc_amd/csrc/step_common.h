@@ -86,20 +86,6 @@ struct LayerK {
   int32_t cmp;           // row-group backward after the fused forward (step_fused_fwd): every
                          // F_l is complete in slice 0 of its partial buffer (one load, not 16)
   unsigned long long* stamps;  // -DDGPRF_STAMPS diagnostic build: stamp buffer, else null
-  // folded SGHMC update (k_step_bwd<..., IPU = true>, plan.ipu): the last of a slice's row-tile
-  // workgroups to arrive updates that slice of W_l and its momenta in place
-  float* mom;            // momenta of W_l, chain 0 (chain stride w_cs)
-  const float* mass;     // [C][n_layers]
-  const int64_t* step;
-  unsigned* cnt;         // this layer's slice arrival counters, chain 0 (chain stride ws_cs words)
-  uint64_t seed;
-  UpdateDev ud;
-  int32_t w_off, w_len, n_layers, step_offset;
-  // step t+1's minibatch rows gathered by gather_blocks extra workgroups (layer-0 forward)
-  BatchDev bd;
-  float* xb_next;        // chain 0 (chain stride ws_cs)
-  float* yb_next;
-  int32_t gather_blocks, yb_cols;
 };
 
 // A_1 elements at p: slab 0 + slab 1 of the GEMM's two K parts (sl = 0: one slab).  Every layer-0
@@ -468,116 +454,6 @@ __device__ __forceinline__ void step_schedule(const UpdateDev& ud, int64_t t, fl
 }
 
 
-// Extra workgroups of the layer-0 forward (a.gather_blocks): step t+1's minibatch rows into the
-// other gathered-rows buffer, off the step's critical path (the buffer this step reads is not
-// touched).  Wide rows (d_in > GATHER_WIDE) one wave each, else one thread each.
-__device__ __forceinline__ void gather_next_rows(const LayerK& a, int gb) {
-  const int chain = blockIdx.z;
-  const int64_t t = *a.step + (int64_t)a.step_offset + 1;
-  float* xb = a.xb_next + (int64_t)chain * a.ws_cs;
-  float* yb = a.yb_next + (int64_t)chain * a.ws_cs;
-  if (a.d_in > GATHER_WIDE) {
-    const int b = gb * (int)(blockDim.x >> 6) + (int)(threadIdx.x >> 6);
-    if (b < a.B) gather_row_wave(a.bd, a.B, a.d_in, a.yb_cols, xb, yb, chain, t, b, threadIdx.x & 63);
-    return;
-  }
-  const int b = gb * (int)blockDim.x + (int)threadIdx.x;
-  if (b < a.B) gather_row(a.bd, a.B, a.d_in, a.yb_cols, xb, yb, chain, t, b);
-}
-
-// 16-byte load that bypasses this CU's L1 (cache policy sc1): data another workgroup stored
-// write-through and handed off by an agent-scope counter (MI355X_MICROARCH.md, Valid forms row 1)
-__device__ __forceinline__ f4 bload4_sc1(rsrc_t r, uint32_t byte_off) {
-  return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16));
-}
-
-// Folded SGHMC update of one feature slice of W_l (plan.ipu; models/dgp.py:206-216), run by every
-// workgroup of the per-row-tile backward once its gW partial row (stored write-through) and its
-// dX partial are out.  Hand-off (MI355X_MICROARCH.md §Workgroup dispatch, Valid forms row 1):
-// every wave drains its stores, a workgroup barrier, then ONE agent-scope add per workgroup on the
-// slice's counter; the workgroup whose add returns n_rt - 1 is the last, resets the counter (so it
-// is zero for the next launch), and after a barrier its waves read the n_rt partial rows with sc1
-// loads.  Each of its lanes then owns packed-parameter quads of the slice: the partial rows summed
-// in row-tile order from zero, the prior term W/N, and the update of w_update_quad — the same
-// operations in the same order as the update kernel, so both forms give identical bits.  The
-// slice's W rows are read only by this slice's workgroups of this launch, all of which have
-// arrived.  `flag`: one LDS word no wave uses any more.
-template <bool RBF>
-__device__ __forceinline__ void ipu_slice(const LayerK& a, int chain, int sl, int* flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  unsigned* cnt = a.cnt + (int64_t)chain * a.ws_cs + sl;
-  if (threadIdx.x == 0) {
-    const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const bool last = old == (unsigned)(a.n_rt - 1);
-    if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *flag = last ? 1 : 0;
-  }
-  __syncthreads();
-  if (*flag == 0) return;
-  const UpdateDev& ud = a.ud;
-  const int R = a.R, g = a.g, nf = 64 * a.cpw;
-  const int fb0 = sl * nf, fe = min(fb0 + nf, R);
-  const int64_t t = *a.step + (int64_t)a.step_offset;
-  const float M = a.mass[chain * a.n_layers + a.layer];
-  const int64_t cw = (int64_t)chain * a.w_cs;
-  float* th_base = const_cast<float*>(a.W) + cw;
-  float* m_base = a.mom + cw;
-  const rsrc_t rth = make_rsrc(th_base, a.w_len);
-  const rsrc_t rm = make_rsrc(m_base, a.w_len);
-  const rsrc_t rs = make_rsrc(a.gwp + (int64_t)chain * a.ws_cs, (int64_t)a.n_rt * a.w_cs);
-  // the slice's parameter quads: half h covers layer elements [(hR + fb0) g, (hR + fe) g)
-  const int qa0 = (fb0 * g) >> 2, qb0 = (fe * g + 3) >> 2;
-  const int qa1 = ((R + fb0) * g) >> 2, qb1 = ((R + fe) * g + 3) >> 2;
-  const int n0 = qb0 - qa0, ntot = n0 + (RBF ? qb1 - qa1 : 0);
-  float lr, T;
-  int resample;
-  if (ud.schedule == DGPRF_SCHED_CYCLICAL) step_schedule<true>(ud, t, &lr, &T, &resample);
-  else step_schedule<false>(ud, t, &lr, &T, &resample);
-  const float N = ud.data_size, beta = ud.beta, h = sqrtf(lr / N);
-  for (int i = threadIdx.x; i < ntot; i += blockDim.x) {
-    const bool h1 = i >= n0;
-    const int q = h1 ? qa1 + (i - n0) : qa0 + i;
-    const int ea = ((h1 ? R : 0) + fb0) * g, eb = ((h1 ? R : 0) + fe) * g;
-    const int e0 = 4 * q;
-    const uint32_t off = (uint32_t)e0 * 4u;
-    const f4 th = bload4(rth, off);
-    f4 m = bload4(rm, off);
-    f4 v[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j)
-      v[j] = bload4_sc1(rs, j < a.n_rt ? (uint32_t)(((int64_t)j * a.w_cs + e0) * 4) : DGPRF_OOB);
-    f4 sacc = f4zero();
-#pragma unroll
-    for (int j = 0; j < 16; ++j) sacc += v[j];
-    const f4 gr = th / N + sacc;  // dU/dW = W/N + Phi^T dF (models/dgp.py:129-136,171)
-    const int64_t eg = (int64_t)a.w_off + e0;  // packed index: Philox quad, injected-noise slot
-    const uint32_t quad = (uint32_t)(eg >> 2);
-    if (resample) {
-      if (ud.xi_resample)
-        m = bload4(make_rsrc(ud.xi_resample + (int64_t)chain * (a.w_cs) + a.w_off, a.w_len), off);
-      else
-        m = philox_normal4(a.seed, (uint64_t)t, DGPRF_RNG_RESAMPLE, (uint32_t)chain, quad);
-    }
-    f4 mn = beta * m - (h * N) * gr;
-    const f4 eps = ud.xi ? bload4(make_rsrc(ud.xi + (int64_t)chain * a.w_cs + a.w_off, a.w_len), off)
-                         : philox_normal4(a.seed, (uint64_t)t, DGPRF_RNG_NOISE, (uint32_t)chain, quad);
-    mn = mn + sqrtf(2.0f * (1.0f - beta) * T * M) * eps;
-    const f4 thn = th + (h * (1.0f / M)) * mn;
-    if (e0 >= ea && e0 + 3 < eb) {
-      *reinterpret_cast<f4*>(m_base + e0) = mn;
-      *reinterpret_cast<f4*>(th_base + e0) = thn;
-    } else {
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (e0 + k >= ea && e0 + k < eb) {
-          m_base[e0 + k] = mn[k];
-          th_base[e0 + k] = thn[k];
-        }
-    }
-  }
-}
-
 // One lane's four packed parameters e0..e0+3 (one counter quad of Philox normals, 16-byte loads;
 // layer offsets are multiples of 4, so a quad never straddles two layers): the row-tile gW partials
 // summed in a fixed order, the prior term W/N, and m <- b m - h N g + sqrt(2(1-b) T M) xi,
@@ -681,8 +557,8 @@ inline LayerK make_layer_k(const dgprf_plan_t& pl, const StepDev& sd, int l, int
   a.dxout = l > 0 ? sd.ws + pl.dxp_off[l] : sd.ws;
   a.gwp = sd.ws + pl.gwp_off + pl.w_off[l];
   a.logp = sd.ws + pl.logp_off;
-  a.xrows = direct ? sd.bd.X : sd.xb;
-  a.yrows = direct ? sd.bd.Y : sd.yb;
+  a.xrows = direct ? sd.bd.X : sd.ws + pl.xb_off;
+  a.yrows = direct ? sd.bd.Y : sd.ws + pl.yb_off;
   a.xrow_cs = direct ? 0 : pl.ws_chain;
   a.yrow_cs = direct ? 0 : pl.ws_chain;
   a.y_cols = direct ? sd.bd.y_cols : pl.yb_cols;
@@ -759,21 +635,6 @@ inline LayerK make_layer_k(const dgprf_plan_t& pl, const StepDev& sd, int l, int
   a.rw_one = a.cmp = 0;
   a.rw_orows = a.rw_pad = 0;
   a.stamps = nullptr;
-  a.mom = sd.mom + pl.w_off[l];
-  a.mass = sd.mass;
-  a.step = sd.step;
-  a.cnt = sd.ws ? reinterpret_cast<unsigned*>(sd.ws + pl.cnt_off) + l * NSM : nullptr;
-  a.seed = sd.seed;
-  a.ud = sd.ud;
-  a.w_off = (int32_t)pl.w_off[l];
-  a.w_len = (int32_t)((int64_t)pl.P[l] * pl.n_gp[l]);
-  a.n_layers = pl.n_layers;
-  a.step_offset = sd.step_offset;
-  a.bd = sd.bd;
-  a.xb_next = sd.xb_next;
-  a.yb_next = sd.yb_next;
-  a.gather_blocks = 0;
-  a.yb_cols = pl.yb_cols;
   return a;
 }
 
@@ -883,8 +744,8 @@ template <int KS>
 void k_step_fwd_launch2(int g, bool rbf, int nw, dim3 grid, size_t lds, hipStream_t s,
                         const LayerK& a);
 template <int KS>
-void k_step_bwd_launch2(int g, bool rbf, bool fb, bool w8, bool ipu, dim3 grid, size_t lds,
-                        hipStream_t s, const LayerK& a);
+void k_step_bwd_launch2(int g, bool rbf, bool fb, bool w8, dim3 grid, size_t lds, hipStream_t s,
+                        const LayerK& a);
 template <int KS>
 void k_step_bwd_rw_launch2(int g, bool rbf, bool fb, bool dx, int nch, int nwv, dim3 grid, size_t lds,
                            hipStream_t s, const LayerK& a);

@@ -9,10 +9,6 @@ namespace dgprf_sk {
 template <int KS, int NOT, bool RBF, bool G1, int NWB>
 __global__ __launch_bounds__(64 * NWB) void k_step_fwd(const LayerK a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  if ((int)blockIdx.x >= a.main_blocks) {  // layer 0 of a graph step: step t+1's rows
-    gather_next_rows(a, (int)blockIdx.x - a.main_blocks);
-    return;
-  }
   int rt, sl;
   if (!tile_of_block(a, rt, sl)) return;
   const int chain = blockIdx.z;

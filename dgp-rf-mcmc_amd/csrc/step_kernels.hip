@@ -531,13 +531,13 @@ void k_step_fwd_launch(int d, int g, bool rbf, int nw, dim3 grid, size_t lds, hi
   else k_step_fwd_launch2<0>(g, rbf, nw, grid, lds, s, a);
 }
 
-void k_step_bwd_launch(int d, int g, bool rbf, bool fb, bool w8, bool ipu, dim3 grid, size_t lds,
+void k_step_bwd_launch(int d, int g, bool rbf, bool fb, bool w8, dim3 grid, size_t lds,
                        hipStream_t s, const LayerK& a) {
-  if (d <= 4) k_step_bwd_launch2<1>(g, rbf, fb, w8, ipu, grid, lds, s, a);
-  else if (d <= 8) k_step_bwd_launch2<2>(g, rbf, fb, w8, ipu, grid, lds, s, a);
-  else if (d <= 16) k_step_bwd_launch2<4>(g, rbf, fb, w8, ipu, grid, lds, s, a);
-  else if (d <= 32) k_step_bwd_launch2<8>(g, rbf, fb, w8, ipu, grid, lds, s, a);
-  else k_step_bwd_launch2<0>(g, rbf, fb, w8, ipu, grid, lds, s, a);
+  if (d <= 4) k_step_bwd_launch2<1>(g, rbf, fb, w8, grid, lds, s, a);
+  else if (d <= 8) k_step_bwd_launch2<2>(g, rbf, fb, w8, grid, lds, s, a);
+  else if (d <= 16) k_step_bwd_launch2<4>(g, rbf, fb, w8, grid, lds, s, a);
+  else if (d <= 32) k_step_bwd_launch2<8>(g, rbf, fb, w8, grid, lds, s, a);
+  else k_step_bwd_launch2<0>(g, rbf, fb, w8, grid, lds, s, a);
 }
 
 }  // namespace dgprf_sk
@@ -612,11 +612,7 @@ hipError_t launch_step_fwd(const dgprf_plan_t& pl, const StepDev& sd, int layer,
     const hipError_t e = launch_step_agemm(pl, sd, s);
     if (e != hipSuccess) return e;
   }
-  // layer 0 of a graph step: extra workgroups gather step t+1's rows into the other buffer
-  if (layer == 0 && sd.gather_next && sd.bd.mode == DGPRF_BATCH_EPOCH && sd.ws)
-    a.gather_blocks = pl.d_in > GATHER_WIDE ? (pl.batch + nwf - 1) / nwf
-                                            : (pl.batch + 64 * nwf - 1) / (64 * nwf);
-  dim3 grid(a.main_blocks + a.gather_blocks, 1, pl.n_chains);
+  dim3 grid(a.main_blocks, 1, pl.n_chains);
   k_step_fwd_launch(pl.d[layer], pl.n_gp[layer], pl.kind[layer] == DGPRF_RBF, nwf, grid,
                     (size_t)lds_floats * sizeof(float), s, a);
   return hipGetLastError();
@@ -627,7 +623,7 @@ hipError_t launch_step_fwd_fused(const dgprf_plan_t& pl, const StepDev& sd, hipS
   float* f_out[DGPRF_MAX_LAYERS];
   for (int l = 0; l < DGPRF_MAX_LAYERS; ++l) f_out[l] = l < pl.n_layers ? sd.ws + pl.fp_off[l] : nullptr;
   const bool direct = sd.bd.mode == DGPRF_BATCH_DIRECT;
-  const float* X = direct ? sd.bd.X : sd.xb;
+  const float* X = direct ? sd.bd.X : sd.ws + pl.xb_off;
   // random_fixed=False layers: this step's Omega is the workspace copy (k_fresh_omega)
   const float* om = pl.fresh_z && pl.omf_off >= 0 ? sd.ws + pl.omf_off : sd.omega;
   return launch_forward_rows(pl, sd.theta, om, sd.der, X, nullptr, 0, pl.batch, f_out, nullptr,
@@ -717,11 +713,8 @@ hipError_t launch_step_bwd(const dgprf_plan_t& pl, const StepDev& sd, int layer,
     a = make_layer_k(pl, sd, layer, lds_floats, /*bwd=*/true, 4);
   }
   dim3 grid(a.main_blocks, 1, pl.n_chains);
-  // the folded update (plan.ipu): W-only steps of the per-row-tile backward, counters in the
-  // workspace (32-bit buffer offsets, host-checked by dgprf_plan_init)
-  const bool ipu = sd.ipu && pl.ipu && !sd.full_bayes;
   k_step_bwd_launch(pl.d[layer], pl.n_gp[layer], pl.kind[layer] == DGPRF_RBF, sd.full_bayes != 0,
-                    w8, ipu, grid, (size_t)lds_floats * sizeof(float), s, a);
+                    w8, grid, (size_t)lds_floats * sizeof(float), s, a);
   return hipGetLastError();
 }
 
@@ -757,8 +750,8 @@ hipError_t launch_step_update(const dgprf_plan_t& pl, const StepDev& sd, const U
   a.d_in = pl.d_in;
   a.yb_cols = pl.yb_cols;
   a.bd = sd.bd;
-  a.xb = sd.xb_next;  // the other gathered-rows buffer (gather_next)
-  a.yb = sd.yb_next;
+  a.xb = sd.ws ? sd.ws + pl.xb_off : nullptr;
+  a.yb = sd.ws ? sd.ws + pl.yb_off : nullptr;
   const int64_t quads = ((int64_t)a.e_end + 3) / 4;
   a.upd_blocks = (int)((quads + UPD_THREADS - 1) / UPD_THREADS);
   const bool gin = grad_in != nullptr, gonly = ud.grad_only != 0;
@@ -865,8 +858,8 @@ hipError_t launch_gather(const dgprf_plan_t& pl, const StepDev& sd, hipStream_t 
   GatherK a;
   a.bd = sd.bd;
   a.step = sd.step;
-  a.xb = sd.xb;
-  a.yb = sd.yb;
+  a.xb = sd.ws + pl.xb_off;
+  a.yb = sd.ws + pl.yb_off;
   a.ws_cs = pl.ws_chain;
   a.B = pl.batch;
   a.d_in = pl.d_in;

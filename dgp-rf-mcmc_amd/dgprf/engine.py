@@ -155,7 +155,6 @@ class Engine:
         self._fwd_scratch = None
         self._plan_tensors = {}
         self.moments_ready = False
-        self.sep_update = False  # True: the separate update kernel even where plan.ipu folds it
 
     # ---------------------------------------------------------------- views
     def W_view(self, l, chain=0):
@@ -278,12 +277,11 @@ class Engine:
             pl = self.spec.plan(key[0], self.C, self.per_chain_hyp)
             # fresh z layers; a forward path pinned by set_forward_path also pins the step's
             # all-layer forward (large minibatches)
-            if fresh_z or full_bayes or self.layout.fwd_path != N.FWD_AUTO or self.sep_update:
+            if fresh_z or full_bayes or self.layout.fwd_path != N.FWD_AUTO:
                 pl.fresh_z = key[1]
                 pl.bwd_tiles = int(key[2])
                 pl.fwd_path = self.layout.fwd_path
                 pl.agemm_chunk_rows = self.layout.agemm_chunk_rows
-                pl.sep_update = int(self.sep_update)
                 N.call("dgprf_plan_init", ctypes.byref(pl))
             ws = torch.zeros(max(pl.ws_total, 4), dtype=_F32, device=self.dev)
             self._ws[key] = (pl, ws)
@@ -552,15 +550,6 @@ class Engine:
         if self._fwd_scratch is None or self._fwd_scratch.numel() < need.value:
             self._fwd_scratch = torch.empty(need.value, dtype=_F32, device=self.dev)
         return self._fwd_scratch
-
-    def set_separate_update(self, flag=True):
-        """Run W-only steps with the separate update kernel even where the plan folds the update
-        into the backward (plan.ipu) — parity of both forms and A/B timing; default False."""
-        torch.cuda.current_stream(self.dev).synchronize()
-        self.sep_update = bool(flag)
-        self._ws.clear()
-        self._graphs.clear()
-        self._plan_tensors.clear()
 
     def set_forward_path(self, path=N.FWD_AUTO, agemm_chunk_rows=0):
         """Pin the predictive forward path (N.FWD_*) and the A_1 chunk size — parity tests of

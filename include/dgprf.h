@@ -25,12 +25,11 @@
 extern "C" {
 #endif
 
-#define DGPRF_ABI_VERSION 8
+#define DGPRF_ABI_VERSION 7
 
 #define DGPRF_MAX_LAYERS 8
 #define DGPRF_MAX_G 64        /* max latent GPs per layer (n_gp[l]) */
 #define DGPRF_MAX_D 2048      /* max layer input width d_l */
-#define DGPRF_IPU_MAX_SLICE 2048 /* max parameters of one feature slice for the folded update */
 
 /* kernel types: models/dgp.py:80-90 (kernel_type_list entries 'RBF' / 'ARC') */
 #define DGPRF_RBF 0
@@ -131,9 +130,6 @@ typedef struct dgprf_plan {
                               whatever B.  For full_bayesian=True steps / gradients at B > 256 when
                               some layer does not fit the full-Bayes row-group layout
                               (rg_full_bayes == 0, e.g. BASELINE config 4's 784-wide layer); ABI 7 */
-  int32_t sep_update;      /* 1: keep the separate update kernel even where the backward can fold
-                              the SGHMC update in (plan.ipu); for A/B timing and parity of both
-                              forms.  ABI 8 */
   /* ---- derived by dgprf_plan_init ---- */
   int32_t initialised;
   int32_t d[DGPRF_MAX_LAYERS];      /* layer input width */
@@ -151,16 +147,7 @@ typedef struct dgprf_plan {
   int32_t rg_full_bayes;            /* rt_per_group > 1: every layer also fits the full-Bayes
                                        row-group backward (else full_bayes steps / gradients
                                        return DGPRF_E_SHAPE for this batch size)                */
-  int32_t ipu;                      /* 1: W-only SGHMC steps fold the update into the backward: the
-                                       last of a feature slice's row-tile workgroups to arrive (one
-                                       agent-scope counter per slice) sums the slice's gW partial
-                                       rows in row-tile order and applies models/dgp.py:206-216 to
-                                       that slice's W and momenta in place (no update launch).  Set
-                                       when the per-row-tile backward runs (B <= 256), every slice
-                                       holds <= DGPRF_IPU_MAX_SLICE parameters and !sep_update.
-                                       ABI 8 */
   int32_t pad1;
-  int32_t pad2;
   int64_t omega_off[DGPRF_MAX_LAYERS];
   int64_t w_off[DGPRF_MAX_LAYERS];
   int64_t lis_off[DGPRF_MAX_LAYERS];
@@ -188,12 +175,6 @@ typedef struct dgprf_plan {
                                         MFMA GEMM per step (per chain); -1 when not used          */
   int64_t omf_off;                   /* fresh_z != 0: this step's Omega of every layer [omega_total]
                                         (per chain; fresh layers rebuilt each step); -1 otherwise */
-  int64_t xb2_off;                   /* second gathered-rows buffer X [B][d_in] (per chain): step k
-                                        of a graph reads buffer k % 2 while the first kernel of that
-                                        step gathers step k + 1's rows into the other.  ABI 8    */
-  int64_t yb2_off;                   /* its targets [B][yb_cols]                                */
-  int64_t cnt_off;                   /* uint32 arrival counters [DGPRF_MAX_LAYERS][16] of the
-                                        folded update (plan.ipu; per chain, zero between launches) */
 } dgprf_plan_t;
 
 /* Device state of the chains.  Replaces the tf.Variables W and their ad-hoc attributes

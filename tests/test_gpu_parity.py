@@ -335,46 +335,6 @@ def test_graph_replay_equals_eager_steps(dev):
     assert torch.equal(a._engine.mom, b._engine.mom)
 
 
-@pytest.mark.parametrize("spg", [5, 8])
-def test_folded_update_graphs_equal_eager_and_separate_update(dev, spg):
-    """plan.ipu: W-only steps fold the SGHMC update into the backward (the last of a slice's row
-    tiles to arrive updates the slice in place) and the layer-0 forward gathers step t+1's rows
-    into the other of two row buffers.  Graph replays of spg steps (odd spg: the buffer parity
-    restarts with every replay) equal eager steps bit for bit, and the folded form equals the
-    separate update kernel (sep_update) to fp32 rounding over 15 steps."""
-    from likelihoods import Gaussian
-    from models.regression_model import RegressionDGP
-    from dgprf import engine as E
-    mk = lambda: RegressionDGP(8, 1, n_hidden_layers=3, n_rf=256, n_gp=[8, 8, 1],
-                               likelihood=Gaussian(variance=0.1))
-    models = []
-    for _ in range(3):
-        E.set_seed(41)
-        models.append(mk())
-    a, b, c = models
-    assert a._engine.plan_ws(200)[0].ipu == 1
-    n = 4000
-    X = torch.randn(n, 8, device=dev)
-    Y = torch.randn(n, 1, device=dev)
-    for mm in models:
-        mm.precond_update(None, n, precond_type="identity")
-    for mm in (b, c):
-        mm._engine.mom.copy_(a._engine.mom)
-    c._engine.set_separate_update(True)
-    assert c._engine.plan_ws(200)[0].ipu == 0
-    run = dict(batch_size=200, lr=0.01, momentum_decay=0.9, steps_per_graph=spg, perm_seed=6)
-    a.run_sgmcmc(X, Y, n, 15, **run)
-    c.run_sgmcmc(X, Y, n, 15, **run)
-    for _ in range(15):
-        b._engine.step(X, Y, n, 0.01, 0.9, 1.0, batch_size=200, mode=2, perm_seed=6)
-    torch.cuda.synchronize()
-    assert torch.equal(a._engine.theta, b._engine.theta)
-    assert torch.equal(a._engine.mom, b._engine.mom)
-    scale = float(a._engine.theta.abs().max())
-    assert float((a._engine.theta - c._engine.theta).abs().max()) <= 1e-5 * scale
-    assert torch.isfinite(a._engine.theta).all()
-
-
 def test_per_call_sgmcmc_update_equals_graph_replays(dev):
     """The reference's driver loop — one model.sgmcmc_update(x, y, N, ...) call per minibatch
     (experiments/utils_training.py:45-61 -> models/dgp.py:184-216) — is bit-equal over 10 steps to
