@@ -490,21 +490,39 @@ def main():
     steps_per_s = world * args.steps / t_steps
 
     # ---------------- predictive samples (full test forward + log p + se + LSE fold)
+    # The driver scores posterior samples it has collected (utils_training.py:79-85): two samples
+    # per pass (PredictiveLSE.add_samples -> the pair kernel, layer 0 shared since Omega is fixed),
+    # here the chain's W now and one SGHMC step later.  The one-sample launch is timed beside it.
+    th_pair = [model._engine.theta.clone()]
+    model.run_sgmcmc(X, Y, N_, 1, **run)
+    th_pair.append(model._engine.theta.clone())
+    th_pair = torch.stack(th_pair)  # [2, 1, w_total]
+    n_pairs = max(1, args.pred_samples // 2)
     acc = PredictiveLSE(model._engine, Xt, Yt)
-    acc.add_sample()
-    acc.add_sample()
+    acc.add_samples(th_pair)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier_sync()
     t0 = time.perf_counter()
     ev0.record()
-    for _ in range(args.pred_samples):
-        acc.add_sample(build=False)
+    for _ in range(n_pairs):
+        acc.add_samples(th_pair, build=False)
     ev1.record()
     ll, rmse = acc.finalize(y_std=1.0)
     barrier_sync()
     t_pred = max_over_ranks(time.perf_counter() - t0)
-    pred_kernel_ms = ev0.elapsed_time(ev1) / args.pred_samples
-    pred_per_s = world * args.pred_samples / t_pred
+    pred_kernel_ms = ev0.elapsed_time(ev1) / (2 * n_pairs)  # per sample
+    pred_per_s = world * 2 * n_pairs / t_pred
+    acc1 = PredictiveLSE(model._engine, Xt, Yt)
+    acc1.add_sample(build=False)
+    ev2, ev3 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    ev2.record()
+    for _ in range(10):
+        acc1.add_sample(build=False)
+    ev3.record()
+    torch.cuda.synchronize()
+    single_ms = ev2.elapsed_time(ev3) / 10
+    del acc1
 
     # ---------------- per-kernel device times (hipEvents on the launch stream) -> roofline
     eng = model._engine
@@ -582,17 +600,31 @@ def main():
             "inflow_event_us": [round(x * 1e3, 3) for x in inflow],
             "update_hbm_GBps": round(upd_bytes / (att_upd * 1e-3) / 1e9, 2),
             "regime": "latency-bound at B=200: 51.6 MFLOP/step; see DESIGN.md"}
-    fp = pred_flops(CFG["N_test"], d, R, P, g)
-    n_trans = CFG["N_test"] * sum(2 * r for r in R)  # sin + cos per RBF feature per test row
-    roof_pred = {"kernel": "k_forward_tiles", "bound": "mfma",
+    fp1 = pred_flops(CFG["N_test"], d, R, P, g)
+    # executed per sample in a pair pass: layer 0's A = X Omega_1 once for the two samples
+    fp = fp1 - CFG["N_test"] * d[0] * R[0]
+    # sin + cos per RBF feature per test row (layer 0's once per pair)
+    n_trans = CFG["N_test"] * (R[0] + sum(2 * r for r in R[1:]))
+    roof_pred = {"kernel": "k_forward_pairs", "bound": "mfma",
                  "achieved": round(fp / (pred_kernel_ms * 1e-3) / 1e12, 4),
                  "peak": FP32_MFMA_PEAK / 1e12, "unit": "TFLOP/s",
                  "frac": round(fp / (pred_kernel_ms * 1e-3) / FP32_MFMA_PEAK, 5),
-                 "traffic": pmc_traffic("k_forward_tiles"),
+                 "traffic": pmc_traffic("k_forward_pairs"),
+                 "traffic_per": "launch (two samples)",
                  "algorithmic_bytes": int(4 * CFG["N_test"] * (CFG["D"] + 1 + 3 * 2)),
-                 "avg_launch_us": round(pred_kernel_ms * 1e3, 2),
-                 "rocprof_avg_launch_us": rocprof_avg_us("k_forward_tiles"),
-                 "flops_per_launch": int(fp),
+                 "avg_us_per_sample": round(pred_kernel_ms * 1e3, 2),
+                 "avg_launch_us": round(2 * pred_kernel_ms * 1e3, 2),
+                 "rocprof_avg_launch_us": rocprof_avg_us("k_forward_pairs"),
+                 "flops_per_sample": int(fp),
+                 "flops_per_launch": int(2 * fp),
+                 "flops_note": "executed FLOPs: SURVEY §8d's per-sample count minus layer 0's "
+                               "X Omega_1 once per pair (one A-tile pass serves both samples)",
+                 "samples_per_launch": 2,
+                 "single_sample": {"kernel": "k_forward_tiles",
+                                   "us_per_sample": round(single_ms * 1e3, 2),
+                                   "frac": round(fp1 / (single_ms * 1e-3) / FP32_MFMA_PEAK, 5),
+                                   "rocprof_avg_launch_us": rocprof_avg_us("k_forward_tiles"),
+                                   "traffic": pmc_traffic("k_forward_tiles")},
                  "transcendental_ceiling": {
                      "sin_cos_per_sample": int(n_trans), "rate_per_s": TRANS_PER_S,
                      "floor_us": round(n_trans / TRANS_PER_S * 1e6, 2),

@@ -490,6 +490,24 @@ int dgprf_forward(const dgprf_plan_t* plan, const float* theta, const float* ome
                                            se, lse_m, lse_s, se_sum, scratch, as_stream(stream)));
 }
 
+int dgprf_forward_samples(const dgprf_plan_t* plan, const float* thetas, int32_t n_samples,
+                          const float* omega, const float* der, const float* X, const float* Y,
+                          int32_t y_cols, int64_t n, float* lse_m, float* lse_s, float* se_sum,
+                          float* scratch, int64_t scratch_floats, void* stream) {
+  int rc = check_plan(plan);
+  if (rc) return rc;
+  if (!thetas || n_samples < 1 || !omega || !der || n < 0 || (n > 0 && (!X || !Y)) || y_cols < 1 ||
+      !lse_m || !lse_s)
+    return DGPRF_E_ARG;
+  if (se_sum && plan->likelihood != DGPRF_LIK_GAUSSIAN) return DGPRF_E_ARG;
+  if (plan->likelihood == DGPRF_LIK_GAUSSIAN && y_cols < plan->n_gp[plan->n_layers - 1])
+    return DGPRF_E_SHAPE;
+  if (scratch_floats < 0 || (scratch_floats > 0 && !scratch)) return DGPRF_E_ARG;
+  if (scratch_floats < dgprf::forward_cfg(*plan, n).scratch_floats) return DGPRF_E_ARG;
+  return hip_rc(dgprf::launch_forward_samples(*plan, thetas, n_samples, omega, der, X, Y, y_cols, n,
+                                              lse_m, lse_s, se_sum, scratch, as_stream(stream)));
+}
+
 int dgprf_lse_finalize(const float* lse_m, const float* lse_s, const float* se_sum, int32_t parts,
                        int64_t n, double s_total, float log_y_std, float y_std, float* lse_out,
                        double* out, void* stream) {

@@ -526,22 +526,26 @@ struct TileLds {
   int obuf, wbuf, o_off, w_off, xin_off, xin_st, f_off, ftst, total;
 };
 
+// the pair kernel's layer-0 W rows: [half][feature][s * 8 + o], row stride PST (16 + 4: the lanes
+// 16-31 of a read start 16 banks away from lanes 0-15)
+constexpr int PST = 20;
+
 __host__ __device__ inline TileLds tile_lds(const dgprf_plan_t& pl, int notmax, int njo, int tpw,
-                                            bool wide0 = false) {
+                                            bool wide0 = false, int spw = 1) {
   int gmax = 1;
   for (int l = 0; l < pl.n_layers; ++l) gmax = pl.n_gp[l] > gmax ? pl.n_gp[l] : gmax;
   TileLds T;
   T.obuf = 16 * njo * TW_OST;               // njo float4 per thread: 16 Omega rows each
   // [cos|sin][64 features][16 NOT + 4]; notmax = 0 (the lean instance: every layer g <= 8, d <= 8)
   // [cos|sin][64 features][8] (G8) or [cos|sin][64] (g == 1)
-  T.wbuf = notmax == 0 ? 2 * 64 * 8 : 2 * 64 * tw_wst(notmax);
+  T.wbuf = notmax == 0 ? (spw == 2 ? 2 * 64 * PST : 2 * 64 * 8) : 2 * 64 * tw_wst(notmax);
   T.o_off = 0;
   T.w_off = 2 * T.obuf;
   T.xin_st = wide0 ? 4 : round4(pl.d_in);  // wide0: layer 0 reads A_1, no input rows staged
   T.xin_off = T.w_off + 2 * T.wbuf;
   T.ftst = gmax + 1;
   T.f_off = T.xin_off + TWW * tpw * TR * T.xin_st;
-  T.total = T.f_off + TWW * round4(tpw * TR * T.ftst);
+  T.total = T.f_off + TWW * spw * round4(tpw * TR * T.ftst);  // spw samples' F per wave
   return T;
 }
 
@@ -836,6 +840,129 @@ __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
   __syncthreads();  // ftw complete before the next layer reads its x fragments
 }
 
+// Layer 0 of TWO posterior samples at once (pair kernel, lean models: every layer d, g <= 8).
+// Omega_1 and the layer input are the same for every sample — z is drawn once at construction
+// (layers/rf_layers.py:21-22) and the samples differ only in W — so A = X Omega_1 (:42-44) and its
+// cos / sin (or relu) are computed once for both.  The F contraction then has 2 g_0 <= 16 real
+// output columns and runs on v_mfma_f32_16x16x4_f32: A operand = [W_s0 | W_s1]^T (output column
+// i = 8 s + o), B = Phi^T; the 16x16x4 MFMA holds the SIMD issue port for 8 of its 32 cycles where
+// the 4x4x1 blocks of the one-sample body hold it for all of theirs (MI355X_MICROARCH.md).  Both
+// samples' W blocks are staged per 64-feature block in a double-buffered LDS ring with the Omega
+// block; columns o >= g_0 of a sample's eight stay whatever the ring held: they only feed output
+// rows that are never stored.  F_s (scaled by c_1) goes to the wave's F tile of sample s.
+template <bool RBF>
+__device__ __forceinline__ void tile_layer0_pair(const dgprf_plan_t& pl, const float* __restrict__ W0,
+                                                 const float* __restrict__ W1,
+                                                 const float* __restrict__ om, float cl,
+                                                 const TileLds& T, float* smem, const float* xin,
+                                                 float* ftw0, float* ftw1, int lr, int lq) {
+  constexpr int KS = 2;
+  constexpr bool REV = RBF && !DGPRF_PRECISE_TRIG_ON;
+  const int d = pl.d[0], R = pl.n_rf[0], g = pl.n_gp[0];
+  // lane / thread index behind an empty asm (as tile_layer's OPQ): this layer's per-lane offsets
+  // are computed here, not hoisted into registers live through the later layers
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));
+  lr = tid & 15;
+  lq = (tid & 63) >> 4;
+  const int gmag = (1048576 + g - 1) / g;  // floor(e / g) = (e * gmag) >> 20 for e < 4096
+  float xf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    const int col = 4 * ks + lq;
+    xf[ks] = col < d ? xin[lr * T.xin_st + min(col, T.xin_st - 1)] : 0.f;
+  }
+  // one descriptor over both samples' W (W1 - W0 is uniform: C w_total floats, or 0 for an odd
+  // last sample), so no load picks its descriptor per lane
+  const int64_t wn = (int64_t)(RBF ? 2 : 1) * R * g, sd1 = (int64_t)(W1 - W0);
+  const rsrc_t rw = make_rsrc(W0, sd1 + wn);
+  const rsrc_t ro = make_rsrc(om, (int64_t)d * R);
+  const int nh4 = 16 * g;  // float4 of one half's 64-feature block
+  f4 sw[2], so;
+  auto stage_load = [&](int fb) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {  // i < 2 samples x (RBF ? 2 : 1) halves x 16 g
+      const int i = tid + 256 * j, sidx = i >= 2 * nh4, q = i - sidx * 2 * nh4, h = q >= nh4;
+      const int e4 = q - h * nh4;
+      const bool ok = (RBF || h == 0) && i < 4 * nh4;
+      const uint32_t off = (uint32_t)((sidx * sd1 + ((h * R) + fb) * g + 4 * e4) * 4);
+      sw[j] = bload4(rw, ok ? off : DGPRF_OOB);
+    }
+    const int k = tid >> 4, c4 = tid & 15;
+    so = bload4(ro, k < d && fb + 4 * c4 < R ? (uint32_t)((k * R + fb + 4 * c4) * 4) : DGPRF_OOB);
+  };
+  auto stage_store = [&](int buf, int fb) {
+    float* wsb = smem + T.w_off + buf * T.wbuf;
+    float* osb = smem + T.o_off + buf * T.obuf;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int i = tid + 256 * j, sidx = i >= 2 * nh4, q = i - sidx * 2 * nh4, h = q >= nh4;
+      const int e0 = 4 * (q - h * nh4);
+      if ((RBF || h == 0) && i < 4 * nh4) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int e = e0 + t, row = (e * gmag) >> 20, col = e - row * g;
+          if (row < 64) wsb[(h * 64 + row) * PST + 8 * sidx + col] = fb + row < R ? sw[j][t] : 0.f;
+        }
+      }
+    }
+    *reinterpret_cast<f4*>(osb + (tid >> 4) * TW_OST + 4 * (tid & 15)) =
+        REV ? so * 0.15915494309189535f : so;
+  };
+  f4 acc = f4zero(), acs = f4zero();
+  const int nb = (R + 63) >> 6;
+  stage_load(0);
+  stage_store(0, 0);
+  __syncthreads();
+  for (int blk = 0; blk < nb; ++blk) {
+    const int fb = blk * 64, buf = blk & 1;
+    if (blk + 1 < nb) stage_load(fb + 64);
+    const float* wl = smem + T.w_off + buf * T.wbuf + 4 * lq * PST + lr;
+    const float* osb = smem + T.o_off + buf * T.obuf + lq * TW_OST + lr;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      // A[row lr][feature fb + 16c + 4lq + r], shared by both samples
+      f4 at = f4zero();
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) at = mfma16(osb[4 * ks * TW_OST + 16 * c], xf[ks], at);
+      float p0[4], p1[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (REV) {
+          const float u = __builtin_amdgcn_fractf(at[r]);
+          p0[r] = __builtin_amdgcn_cosf(u);
+          p1[r] = __builtin_amdgcn_sinf(u);
+        } else if (RBF) {
+          float sv, cv;
+          rf_sincos(at[r], &sv, &cv);
+          p0[r] = cv;
+          p1[r] = sv;
+        } else {
+          p0[r] = fmaxf(at[r], 0.f);
+          p1[r] = 0.f;
+        }
+      }
+      // F^T[i = 8 s + o][row lr] += W_s[feature][o] Phi[row lr][feature], K = the 4 features of
+      // k-step r (lane group lq holds feature fb + 16c + 4lq + r)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        acc = mfma16(wl[(16 * c + r) * PST], p0[r], acc);
+        if (RBF) acs = mfma16(wl[(64 + 16 * c + r) * PST], p1[r], acs);
+      }
+    }
+    if (blk + 1 < nb) stage_store(buf ^ 1, fb + 64);
+    __syncthreads();
+  }
+  // acc[rr] = F_s[row lr][o] / c for i = 4 lq + rr: s = lq >> 1, o = 4 (lq & 1) + rr
+  float* fs = (lq >> 1) ? ftw1 : ftw0;
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int o = 4 * (lq & 1) + rr;
+    if (o < g) fs[lr * T.ftst + o] = cl * (acc[rr] + acs[rr]);
+  }
+  __syncthreads();  // both samples' F tiles complete before layer 1 reads its x fragments
+}
+
 // Per-wave timeline of the tile kernel for a separate diagnostic build (-DDGPRF_PSTAMPS, never in
 // the product): slot 0 = s_memrealtime at entry, 7 = s_memtime at entry, 1..4 = s_memtime after
 // each layer, 6 = s_memrealtime at exit, 5 = HW_ID | XCC_ID << 32.
@@ -980,6 +1107,102 @@ void k_forward_tiles(
     }
   }
   DGPRF_PST(6, __builtin_amdgcn_s_memrealtime());
+}
+
+// Posterior-predictive scoring of one pair of samples of every chain (thetas [2][C][w_total]; two =
+// false: one sample) for lean models (every layer d, g <= 8; config 2): layer 0 once for the pair
+// (tile_layer0_pair), layers >= 1 and the likelihood per sample, each sample folded into the
+// chain's online log-sum-exp accumulators in sample order (experiments/utils_training.py:79-85).
+// A workgroup covers 64 test rows of one chain, so each accumulator element has one writer.
+// Same register budget as the lean one-sample instance.
+__global__ __launch_bounds__(TW_THREADS) __attribute__((amdgpu_waves_per_eu(TILE_LEAN_WAVES)))
+void k_forward_pairs(const dgprf_plan_t pl, const float* __restrict__ thetas, const int two,
+                     const float* __restrict__ omega, const float* __restrict__ der,
+                     const float* __restrict__ X, const float* __restrict__ Y, const int y_cols,
+                     const int64_t n, float* __restrict__ lse_m, float* __restrict__ lse_s,
+                     float* __restrict__ se_sum) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const TileLds T = tile_lds(pl, 0, 1, 1, false, 2);
+  const int chain = blockIdx.y, C = pl.n_chains;
+  const int64_t ochain = pl.hyp_per_chain ? (int64_t)chain * pl.omega_total : 0;
+  const int64_t dchain = pl.hyp_per_chain ? (int64_t)chain * pl.der_total : 0;
+  // the wave index through readfirstlane: the wave's LDS tiles / row base are SGPR values, not
+  // per-lane registers live through both samples' layers
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, lr = lane & 15, lq = lane >> 4;
+  const int64_t wrow0 = (int64_t)blockIdx.x * TW_ROWS + wave * TR;
+  float* xin = smem + T.xin_off + wave * TR * T.xin_st;
+  float* ftw0 = smem + T.f_off + (2 * wave) * round4(TR * T.ftst);
+  float* ftw1 = smem + T.f_off + (2 * wave + 1) * round4(TR * T.ftst);
+  const int L = pl.n_layers;
+  for (int e = lane; e < TR * T.xin_st; e += 64) {
+    const int r = e / T.xin_st, k = e - r * T.xin_st;
+    const int64_t b = wrow0 + r;
+    xin[e] = (b < n && k < pl.d_in) ? X[b * pl.d_in + k] : 0.f;
+  }
+  for (int e = lane; e < TR * T.ftst; e += 64) ftw0[e] = ftw1[e] = 0.f;
+  __syncthreads();
+  const float* om0 = omega + ochain + pl.omega_off[0];
+  {
+    const float* W0 = thetas + (int64_t)chain * pl.w_total;
+    const float* W1 = two ? W0 + (int64_t)C * pl.w_total : W0;
+    if (pl.kind[0] == DGPRF_RBF)
+      tile_layer0_pair<true>(pl, W0, W1, om0, der[dchain], T, smem, xin, ftw0, ftw1, lr, lq);
+    else
+      tile_layer0_pair<false>(pl, W0, W1, om0, der[dchain], T, smem, xin, ftw0, ftw1, lr, lq);
+    // unrolled: each sample's copy of layers >= 1 keeps only its own state live (a loop over the
+    // two samples spilled 5 VGPRs at the 96-register budget; unrolled: 92, none spilled)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if (j == 1 && !two) break;
+      float* ftw = j ? ftw1 : ftw0;
+      const float* Wc = j ? W1 : W0;
+      for (int layer = 1; layer < L; ++layer) {
+        const float* __restrict__ om = omega + ochain + pl.omega_off[layer];
+        const float* __restrict__ W = Wc + pl.w_off[layer];
+        const float cl = der[dchain + layer];
+        const bool rbf = pl.kind[layer] == DGPRF_RBF;
+        if (pl.n_gp[layer] == 1) {
+          if (rbf) tile_layer<1, true, true, false, 1, 1, 2, 1, false, true>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, n, nullptr);
+          else tile_layer<1, false, true, false, 1, 1, 2, 1, false, true>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, n, nullptr);
+        } else {
+          if (rbf) tile_layer<1, true, false, true, 1, 1, 2, 1, false, true>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, n, nullptr);
+          else tile_layer<1, false, false, true, 1, 1, 2, 1, false, true>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, n, nullptr);
+        }
+      }
+      // likelihood of this sample, folded into the chain's accumulators (as k_forward_tiles)
+      const int64_t b = wrow0 + lr;
+      if (lq == 0 && b < n) {
+        const int g = pl.n_gp[L - 1];
+        const float* f = ftw + lr * T.ftst;
+        const float* y = Y + b * y_cols;
+        float lp = 0.f, se = 0.f;
+        if (pl.likelihood == DGPRF_LIK_GAUSSIAN) {
+          const float var = der[dchain + DGPRF_MAX_LAYERS];
+          const float logvar = logf(var);
+          for (int o = 0; o < g; ++o) {
+            const float diff = y[o] - f[o];
+            lp += -0.5f * (LOG_2PI + logvar + diff * diff / var);
+            se += diff * diff;
+          }
+          se = se / (float)g;
+        } else {
+          float mx = -INFINITY;
+          for (int o = 0; o < g; ++o) mx = fmaxf(mx, f[o]);
+          float sm = 0.f;
+          for (int o = 0; o < g; ++o) sm += expf(f[o] - mx);
+          const int lab = (int)y[0];
+          lp = (lab >= 0 && lab < g) ? f[lab] - (mx + logf(sm)) : __builtin_nanf("");
+        }
+        const int64_t idx = (int64_t)chain * n + b;
+        const float m0 = lse_m[idx], s0 = lse_s[idx];
+        const float m1 = fmaxf(m0, lp);
+        lse_s[idx] = s0 * expf(m0 - m1) + expf(lp - m1);
+        lse_m[idx] = m1;
+        if (se_sum) se_sum[idx] += se;
+      }
+    }
+  }
 }
 
 }  // namespace
@@ -1175,6 +1398,46 @@ hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const
     err = hipGetLastError();
   }
   return err;
+}
+
+// The pair kernel applies where the one-sample path would run the lean tile instance.
+bool forward_pairs_ok(const dgprf_plan_t& pl, int64_t n) {
+  const ForwardCfg cfg = forward_cfg(pl, n);
+  if (!cfg.tiles || cfg.wide0 || TILE_TPW_DEFAULT != 1) return false;
+  for (int l = 0; l < pl.n_layers; ++l)
+    if (pl.n_gp[l] > 8 || pl.d[l] > 8) return false;
+  return true;
+}
+
+hipError_t launch_forward_samples(const dgprf_plan_t& pl, const float* thetas, int n_samples,
+                                  const float* omega, const float* der, const float* X,
+                                  const float* Y, int y_cols, int64_t n, float* lse_m,
+                                  float* lse_s, float* se_sum, float* scratch, hipStream_t s) {
+  if (n <= 0 || n_samples <= 0) return hipSuccess;
+  // 32-bit buffer offsets across two samples' W
+  const bool off_ok = ((int64_t)pl.n_chains * pl.w_total + 2 * (int64_t)pl.n_rf[0] * pl.n_gp[0]) * 4 <
+                      ((int64_t)1 << 31);
+  if (!off_ok || !forward_pairs_ok(pl, n)) {  // one launch per sample (sample order)
+    for (int j = 0; j < n_samples; ++j) {
+      const hipError_t e = launch_forward_rows(pl, thetas + (int64_t)j * pl.n_chains * pl.w_total,
+                                               omega, der, X, Y, y_cols, n, nullptr, nullptr,
+                                               nullptr, lse_m, lse_s, se_sum, scratch, s);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
+  const TileLds T = tile_lds(pl, 0, 1, 1, false, 2);
+  const size_t tl = (size_t)T.total * sizeof(float);
+  dim3 grid((unsigned)((n + TW_ROWS - 1) / TW_ROWS), pl.n_chains);
+  set_lds_limit((const void*)k_forward_pairs, tl);
+  for (int p = 0; p < n_samples; p += 2) {  // one launch per pair of samples
+    hipLaunchKernelGGL(k_forward_pairs, grid, dim3(TW_THREADS), tl, s, pl,
+                       thetas + (int64_t)p * pl.n_chains * pl.w_total, p + 1 < n_samples ? 1 : 0,
+                       omega, der, X, Y, y_cols, n, lse_m, lse_s, se_sum);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 size_t forward_rows_lds_bytes(const dgprf_plan_t& pl) {

@@ -236,17 +236,14 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
 #pragma unroll
   for (int r = 0; r < 4; ++r) dg4[r] = G1 ? dfs[(4 * lq + r) * dfst] : 0.f;
 
-  float* gwp = a.gwp + (int64_t)chain * a.ws_cs + (int64_t)rt * a.w_cs;
-#ifndef DGPRF_GWP_WT
-#define DGPRF_GWP_WT 1
-#endif
   // this row tile's gW partial row, stored write-through (sc1): 13 rows x w_total floats at B = 200
   // that would otherwise sit dirty in the XCD L2s when the launch ends (configs 4 / 5: 12.8 /
   // 13.6 MB per layer; measured config 5 103 -> 98 us/step, config 4 126 -> 124)
-  const rsrc_t rgw = make_rsrc(gwp, a.w_cs);
-  auto gw_store = [&](int64_t i, float v) {
-    if (DGPRF_GWP_WT) bstore1_wt(v, rgw, (uint32_t)(i * 4));
-    else gwp[i] = v;
+  const rsrc_t rgw = make_rsrc(a.gwp + (int64_t)chain * a.ws_cs + (int64_t)rt * a.w_cs, a.w_cs);
+  auto gw_store = [&](int64_t i, float v) { bstore1_wt(v, rgw, (uint32_t)(i * 4)); };
+  auto gw_store4 = [&](int64_t i, f4 v) { bstore4_wt(v, rgw, (uint32_t)(i * 4)); };  // i % 4 == 0
+  auto gw_store2 = [&](int64_t i, float v0, float v1) {  // i % 2 == 0
+    bstore2_wt(v0, v1, rgw, (uint32_t)(i * 4));
   };
   f4 dxa[4] = {f4zero(), f4zero(), f4zero(), f4zero()};
   // full_bayesian=True: per-wave sums over this row tile and the wave's features of
@@ -373,23 +370,36 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
     } else {
 #pragma unroll
       for (int ot = 0; ot < NOT; ++ot) {
+        // dF as the A operand and Phi as B: the tile comes out as gW^T, a lane holding four
+        // consecutive outputs of one feature row, so the partial row is written 16 bytes per lane
+        // (one fabric write per 16 B instead of four dword write-throughs, whole lines per wave)
         f4 gc = f4zero(), gs = f4zero();
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          gc = mfma16(q0[r], dfg[ot][r], gc);
-          if (RBF) gs = mfma16(q1[r], dfg[ot][r], gs);
+          gc = mfma16(dfg[ot][r], q0[r], gc);
+          if (RBF) gs = mfma16(dfg[ot][r], q1[r], gs);
         }
         DGPRF_STAMP(stamp_base, 9);
-        // gc[r] = gW[f0 + 4lq + r][ot*16 + lr]
-        const int o = ot * 16 + lr;
-        if (o < g) {
+        // gc[r] = gW[f0 + lr][ot*16 + 4lq + r]
+        const int o = ot * 16 + 4 * lq, f = f0 + lr;
+        if (o < g && f < R) {
+          if ((g & 3) == 0) {
+            gw_store4((int64_t)f * g + o, gc);
+            if (RBF) gw_store4((int64_t)(R + f) * g + o, gs);
+          } else if ((g & 1) == 0) {  // 8-byte aligned pairs (config 4's g = 30)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int f = f0 + 4 * lq + r;
-            if (f < R) {
-              gw_store((int64_t)f * g + o, gc[r]);
-              if (RBF) gw_store((int64_t)(R + f) * g + o, gs[r]);
-            }
+            for (int r = 0; r < 4; r += 2)
+              if (o + r < g) {
+                gw_store2((int64_t)f * g + o + r, gc[r], gc[r + 1]);
+                if (RBF) gw_store2((int64_t)(R + f) * g + o + r, gs[r], gs[r + 1]);
+              }
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (o + r < g) {
+                gw_store((int64_t)f * g + o + r, gc[r]);
+                if (RBF) gw_store((int64_t)(R + f) * g + o + r, gs[r]);
+              }
           }
         }
       }

@@ -188,6 +188,31 @@ std::tuple<std::vector<Tensor>, Tensor, Tensor> forward(
   return {F, lp, sq};
 }
 
+// thetas [S][C][w_total]: every sample of every chain folded into the LSE accumulators [C][n]
+void forward_samples(const Tensor& plan, const Tensor& thetas, const Tensor& omega,
+                     const Tensor& der, const Tensor& X, const Tensor& Y, const Tensor& lse_m,
+                     const Tensor& lse_s, const OptT& se_sum, const OptT& scratch) {
+  const dgprf_plan_t pl = plan_of(plan);
+  const int64_t C = pl.n_chains, ch = pl.hyp_per_chain ? C : 1;
+  TORCH_CHECK(X.dim() == 2 && X.size(1) == pl.d_in, "dgprf: X must be [n, d_in]");
+  const int64_t n = X.size(0);
+  TORCH_CHECK(Y.dim() == 2 && Y.size(0) == n, "dgprf: Y must be [n, y_cols]");
+  TORCH_CHECK(thetas.dim() == 3 && thetas.size(1) == C && thetas.size(2) == pl.w_total,
+              "dgprf: thetas must be [samples, n_chains, w_total]");
+  const int64_t S = thetas.size(0);
+  int64_t need = 0;
+  check_rc(dgprf_forward_scratch(&pl, n, &need), "dgprf_forward_scratch");
+  float* scr = f32o(scratch, "scratch", need);
+  TORCH_CHECK(need == 0 || scr, "dgprf: forward needs ", need, " floats of scratch");
+  check_rc(dgprf_forward_samples(&pl, f32(thetas, "thetas", S * C * pl.w_total), (int32_t)S,
+                                 f32(omega, "omega", ch * pl.omega_total),
+                                 f32(der, "der", ch * pl.der_total), f32(X, "X"), f32(Y, "Y"),
+                                 (int32_t)Y.size(1), n, f32(lse_m, "lse_m", C * n),
+                                 f32(lse_s, "lse_s", C * n), f32o(se_sum, "se_sum", C * n), scr,
+                                 scr ? scratch->numel() : 0, stream()),
+           "dgprf_forward_samples");
+}
+
 std::tuple<Tensor, Tensor> lse_finalize(const Tensor& m, const Tensor& s, const OptT& e,
                                         double s_total, double y_std, bool lse_out) {
   TORCH_CHECK(m.dim() == 2 && s.sizes() == m.sizes(), "dgprf: accumulators must be [parts, n]");
@@ -222,6 +247,9 @@ TORCH_LIBRARY(dgprf, m) {
       "forward(Tensor plan, Tensor theta, Tensor omega, Tensor der, Tensor X, Tensor? Y, "
       "int f_mask, bool logp, bool se, Tensor(a!)? lse_m, Tensor(b!)? lse_s, Tensor(c!)? se_sum, "
       "Tensor(d!)? scratch) -> (Tensor[], Tensor, Tensor)");
+  m.def(
+      "forward_samples(Tensor plan, Tensor thetas, Tensor omega, Tensor der, Tensor X, Tensor Y, "
+      "Tensor(a!) lse_m, Tensor(b!) lse_s, Tensor(c!)? se_sum, Tensor(d!)? scratch) -> ()");
   m.def("lse_finalize(Tensor m, Tensor s, Tensor? e, float s_total, float y_std, bool lse_out) "
         "-> (Tensor, Tensor)");
 }
@@ -230,5 +258,6 @@ TORCH_LIBRARY_IMPL(dgprf, CUDA, m) {
   m.impl("sghmc_step_", &sghmc_step_);
   m.impl("potential_grad", &potential_grad);
   m.impl("forward", &forward);
+  m.impl("forward_samples", &forward_samples);
   m.impl("lse_finalize", &lse_finalize);
 }

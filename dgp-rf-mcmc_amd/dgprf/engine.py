@@ -540,6 +540,26 @@ class Engine:
             out["se"] = sq
         return out
 
+    def forward_samples(self, thetas, X, Y, lse, omega=None, build=True):
+        """Fold S posterior samples of every chain (thetas [S, C, w_total]) into the LSE
+        accumulators lse = (m, s, se_sum) [C, n] in sample order (dgprf::forward_samples): two
+        samples per pass with layer 0 shared where the model is lean (every layer d, g <= 8)."""
+        X = as_device(X, self.dev)
+        Yd = as_device(Y, self.dev)
+        if Yd.dim() == 1:
+            Yd = Yd[:, None]
+        thetas = as_device(thetas, self.dev)
+        if thetas.dim() == 2:
+            thetas = thetas[:, None, :]
+        if X.dim() != 2 or X.shape[1] != self.spec.d_in:
+            raise ValueError(f"X must be [n, {self.spec.d_in}], got {tuple(X.shape)}")
+        if build:
+            self.build_omega()
+        m, s, e = lse
+        om = self.omega if omega is None else omega
+        ops().forward_samples(self._plan_t(self.layout), thetas, om, self.der, X, Yd, m, s, e,
+                              self.forward_scratch(X.shape[0]))
+
     def forward_scratch(self, n):
         """Engine-owned scratch of dgprf_forward for n rows (the wide-first-layer A_1 chunks),
         grown on demand and reused, so the predictive loop allocates nothing per sample."""

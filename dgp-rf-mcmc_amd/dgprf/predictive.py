@@ -33,6 +33,17 @@ class PredictiveLSE:
         self.eng.forward(self.X, self.Y, lse=(self.m, self.s, self.e), build=build, omega=omega)
         self.S += self.eng.C
 
+    def add_samples(self, thetas, build=True, omega=None):
+        """Score S posterior samples of every chain, thetas [S, C, w_total] (or [S, w_total] for
+        one chain), folded in sample order (dgprf::forward_samples: two samples per pass with the
+        first layer shared for lean models)."""
+        thetas = E.as_device(thetas, self.eng.dev)
+        if thetas.dim() == 2:
+            thetas = thetas[:, None, :]
+        self.eng.forward_samples(thetas, self.X, self.Y, (self.m, self.s, self.e), build=build,
+                                 omega=omega)
+        self.S += thetas.shape[0] * thetas.shape[1]
+
     def finalize(self, y_std=1.0, group=None):
         """(test log-likelihood, RMSE) over every sample of every chain of every rank."""
         m, s, e, S = D.gather_accumulators(self.m, self.s, self.e, self.S, group)

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define DGPRF_ABI_VERSION 7
+#define DGPRF_ABI_VERSION 8
 
 #define DGPRF_MAX_LAYERS 8
 #define DGPRF_MAX_G 64        /* max latent GPs per layer (n_gp[l]) */
@@ -317,6 +317,17 @@ int dgprf_forward(const dgprf_plan_t *plan, const float *theta, const float *ome
  * per point lse[n] = log sum_s exp(lp_s) over all chains' accumulators, and
  * out[0] = mean_n(lse - log S_total) - log_y_std, out[1] = sqrt(sum se / (S_total n)) * y_std.
  * lse_m/lse_s/se_sum are [parts][n] (chains x ranks), combined in fixed order. */
+/* Posterior-predictive fold of several posterior samples of every chain (the driver's loop over W
+ * samples, experiments/utils_training.py:79-85): thetas [n_samples][n_chains][w_total]; each
+ * sample's per-row log p (and squared error) is folded into the chain's online log-sum-exp
+ * accumulators lse_m / lse_s (and se_sum, Gaussian) [n_chains][n] in sample order, as n_samples
+ * dgprf_forward calls would.  Lean models (every layer d, g <= 8, n large enough for the tile
+ * kernel) score two samples per pass with layer 0 computed once for the pair (Omega is fixed across
+ * samples, layers/rf_layers.py:21-22); other models run one forward per sample.  ABI 8. */
+int dgprf_forward_samples(const dgprf_plan_t *plan, const float *thetas, int32_t n_samples,
+                          const float *omega, const float *der, const float *X, const float *Y,
+                          int32_t y_cols, int64_t n, float *lse_m, float *lse_s, float *se_sum,
+                          float *scratch, int64_t scratch_floats, void *stream);
 int dgprf_lse_finalize(const float *lse_m, const float *lse_s, const float *se_sum,
                        int32_t parts, int64_t n, double s_total, float log_y_std, float y_std,
                        float *lse_out, double *out, void *stream);

@@ -60,6 +60,7 @@ def test_secondary_ceilings_present():
     folded = line["roofline"].get("update_folded", False)
     assert lf["launches_per_step"] == (6 if folded else 7) and lf["boundary_us"] > 0
     tc = line["roofline_predictive"]["transcendental_ceiling"]
-    assert tc["sin_cos_per_sample"] == 100_000 * 2 * 3 * 1024
+    # layer 0's cos / sin once per pair of samples (the pair kernel), layers 1-2 per sample
+    assert tc["sin_cos_per_sample"] == 100_000 * (1024 + 2 * 2 * 1024)
     assert 0 < tc["frac_of_sample_time"] < 1
     assert set(line["b_sweep"]) == {"200", "1024", "8192", "65536"}

@@ -98,6 +98,49 @@ def test_predictive_ll_config2_70k_rows_4_samples(dev):
         assert abs(rmse - ref_rmse) < 1e-5 * ref_rmse, (y_std, rmse, ref_rmse)
 
 
+@pytest.mark.parametrize("C,S", [(1, 4), (2, 3)])
+def test_predictive_two_samples_per_launch(dev, C, S):
+    """PredictiveLSE.add_samples (dgprf::forward_samples): config 2's model scores two posterior
+    samples per pass of the pair kernel — layer 0's A = X Omega_1 and cos / sin once for both, its
+    F contraction on 16x16x4 MFMA tiles with the two samples' W side by side — and folds every
+    sample into the chain's accumulators in sample order; an odd S ends with a one-sample pass.
+    LL within 1e-4 and RMSE within 1e-5 relative of the oracle over the C x S samples, and the
+    per-point LSE within 2e-5 of the same samples folded one launch at a time (add_sample)."""
+    from dgprf import _native as N
+    from dgprf import engine as E
+    from dgprf.data import regression_data
+    from dgprf.predictive import PredictiveLSE
+    n_test = 20_001
+    Xt, Yt, _ = regression_data(n_test, CFG2["D"], seed=7, device=dev)
+    m = _config2_model(11)
+    eng = m._engine if C == 1 else _multi_chain_engine(m, C, seed=78)
+    eng.build_omega()
+    E.set_seed(12)
+    thetas = torch.stack([E.normal((C, eng.layout.w_total), N.RNG_W) for _ in range(S)])
+    pair = PredictiveLSE(eng, Xt, Yt)
+    pair.add_samples(thetas, build=False)
+    one = PredictiveLSE(eng, Xt, Yt)
+    keep = eng.theta.clone()
+    for s in range(S):
+        eng.theta.copy_(thetas[s])
+        one.add_sample(build=False)
+    eng.theta.copy_(keep)
+    assert pair.S == one.S == C * S
+    lse_pair = E.lse_finalize(pair.m, pair.s, pair.e, C * S, lse_out=True)[1]
+    lse_one = E.lse_finalize(one.m, one.s, one.e, C * S, lse_out=True)[1]
+    assert torch.all((lse_pair - lse_one).abs() <= 2e-5 * torch.clamp(lse_one.abs(), min=1.0))
+    Xh, Yh = cpu(Xt).astype(np.float64), cpu(Yt).astype(np.float64)
+    lps, ses = [], []
+    for s in range(S):
+        for c in range(C):
+            lp, se = _oracle_lp_se(_oracle_params(m, _unpack(eng, cpu(thetas[s, c]))), Xh, Yh)
+            lps.append(lp)
+            ses.append(se)
+    ll, rmse = pair.finalize(y_std=1.0)
+    ref_ll, ref_rmse = O.predictive_summary(np.stack(lps), np.stack(ses))
+    assert abs(ll - ref_ll) < 1e-4 and abs(rmse - ref_rmse) < 1e-5 * ref_rmse
+
+
 def _multi_chain_engine(m, C, seed):
     """C chains sharing model m's frequencies and hyper-parameters (one posterior)."""
     from dgprf import engine as E
