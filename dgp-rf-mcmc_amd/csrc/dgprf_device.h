@@ -69,11 +69,6 @@ __device__ __forceinline__ float bload1(rsrc_t r, uint32_t byte_off) {
 __device__ __forceinline__ void bstore1_wt(float v, rsrc_t r, uint32_t byte_off) {
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, byte_off, 0, 16);
 }
-typedef unsigned int u32v2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void bstore2_wt(float v0, float v1, rsrc_t r, uint32_t byte_off) {
-  u32v2 v = {__builtin_bit_cast(uint32_t, v0), __builtin_bit_cast(uint32_t, v1)};
-  __builtin_amdgcn_raw_buffer_store_b64(v, r, byte_off, 0, 16);
-}
 typedef unsigned int u32v4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void bstore4_wt(f4 v, rsrc_t r, uint32_t byte_off) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32v4, v), r, byte_off, 0, 16);

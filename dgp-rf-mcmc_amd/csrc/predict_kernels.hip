@@ -526,9 +526,10 @@ struct TileLds {
   int obuf, wbuf, o_off, w_off, xin_off, xin_st, f_off, ftst, total;
 };
 
-// the pair kernel's layer-0 W rows: [half][feature][s * 8 + o], row stride PST (16 + 4: the lanes
-// 16-31 of a read start 16 banks away from lanes 0-15)
-constexpr int PST = 20;
+// the pair kernel's layer-0 W rows: [half][feature][s * 8 + o], row stride PST = 16.  (A stride of
+// 20 puts lanes 16-31 of a read 16 banks away from lanes 0-15, but the ring then pushes the
+// workgroup past 32 KiB of LDS: 4 workgroups per CU instead of the 5 its registers allow.)
+constexpr int PST = 16;
 
 __host__ __device__ inline TileLds tile_lds(const dgprf_plan_t& pl, int notmax, int njo, int tpw,
                                             bool wide0 = false, int spw = 1) {
@@ -543,7 +544,7 @@ __host__ __device__ inline TileLds tile_lds(const dgprf_plan_t& pl, int notmax, 
   T.w_off = 2 * T.obuf;
   T.xin_st = wide0 ? 4 : round4(pl.d_in);  // wide0: layer 0 reads A_1, no input rows staged
   T.xin_off = T.w_off + 2 * T.wbuf;
-  T.ftst = gmax + 1;
+  T.ftst = spw == 2 ? gmax : gmax + 1;  // the pair layout: 5 workgroups' LDS in 160 KiB
   T.f_off = T.xin_off + TWW * tpw * TR * T.xin_st;
   T.total = T.f_off + TWW * spw * round4(tpw * TR * T.ftst);  // spw samples' F per wave
   return T;

@@ -242,9 +242,6 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
   const rsrc_t rgw = make_rsrc(a.gwp + (int64_t)chain * a.ws_cs + (int64_t)rt * a.w_cs, a.w_cs);
   auto gw_store = [&](int64_t i, float v) { bstore1_wt(v, rgw, (uint32_t)(i * 4)); };
   auto gw_store4 = [&](int64_t i, f4 v) { bstore4_wt(v, rgw, (uint32_t)(i * 4)); };  // i % 4 == 0
-  auto gw_store2 = [&](int64_t i, float v0, float v1) {  // i % 2 == 0
-    bstore2_wt(v0, v1, rgw, (uint32_t)(i * 4));
-  };
   f4 dxa[4] = {f4zero(), f4zero(), f4zero(), f4zero()};
   // full_bayesian=True: per-wave sums over this row tile and the wave's features of
   //   hw[k]     = sum_b X[b][k] (dA z^T)[b][k]   (-> log_inv_ls)
@@ -368,40 +365,47 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
         if (RBF) gw_store(R + f, gs);
       }
     } else {
+      // g a multiple of 16 (config 5): dF as the A operand and Phi as B, so the tile comes out as
+      // gW^T — a lane holds four consecutive outputs of one feature row and the partial row is
+      // written 16 bytes per lane (config 5 94.1 -> 93.0 us/step); other widths keep gW's own
+      // orientation and dword stores (16- / 8-byte stores measured slower there: config 2 27.0 ->
+      // 27.4, config 4 108.6 -> 121.8 us/step)
+      const bool t16 = (g & 15) == 0;
 #pragma unroll
       for (int ot = 0; ot < NOT; ++ot) {
-        // dF as the A operand and Phi as B: the tile comes out as gW^T, a lane holding four
-        // consecutive outputs of one feature row, so the partial row is written 16 bytes per lane
-        // (one fabric write per 16 B instead of four dword write-throughs, whole lines per wave)
         f4 gc = f4zero(), gs = f4zero();
+        if (t16) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          gc = mfma16(dfg[ot][r], q0[r], gc);
-          if (RBF) gs = mfma16(dfg[ot][r], q1[r], gs);
-        }
-        DGPRF_STAMP(stamp_base, 9);
-        // gc[r] = gW[f0 + lr][ot*16 + 4lq + r]
-        const int o = ot * 16 + 4 * lq, f = f0 + lr;
-        if (o < g && f < R) {
-          if ((g & 3) == 0) {
+          for (int r = 0; r < 4; ++r) {
+            gc = mfma16(dfg[ot][r], q0[r], gc);
+            if (RBF) gs = mfma16(dfg[ot][r], q1[r], gs);
+          }
+          // gc[r] = gW[f0 + lr][ot*16 + 4lq + r]
+          const int o = ot * 16 + 4 * lq, f = f0 + lr;
+          if (f < R) {
             gw_store4((int64_t)f * g + o, gc);
             if (RBF) gw_store4((int64_t)(R + f) * g + o, gs);
-          } else if ((g & 1) == 0) {  // 8-byte aligned pairs (config 4's g = 30)
+          }
+        } else {
 #pragma unroll
-            for (int r = 0; r < 4; r += 2)
-              if (o + r < g) {
-                gw_store2((int64_t)f * g + o + r, gc[r], gc[r + 1]);
-                if (RBF) gw_store2((int64_t)(R + f) * g + o + r, gs[r], gs[r + 1]);
-              }
-          } else {
+          for (int r = 0; r < 4; ++r) {
+            gc = mfma16(q0[r], dfg[ot][r], gc);
+            if (RBF) gs = mfma16(q1[r], dfg[ot][r], gs);
+          }
+          // gc[r] = gW[f0 + 4lq + r][ot*16 + lr]
+          const int o = ot * 16 + lr;
+          if (o < g) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
-              if (o + r < g) {
-                gw_store((int64_t)f * g + o + r, gc[r]);
-                if (RBF) gw_store((int64_t)(R + f) * g + o + r, gs[r]);
+            for (int r = 0; r < 4; ++r) {
+              const int f = f0 + 4 * lq + r;
+              if (f < R) {
+                gw_store((int64_t)f * g + o, gc[r]);
+                if (RBF) gw_store((int64_t)(R + f) * g + o, gs[r]);
               }
+            }
           }
         }
+        DGPRF_STAMP(stamp_base, 9);
       }
     }
     DGPRF_STAMP(stamp_base, 6);

@@ -9,6 +9,7 @@ for rep in $(seq 1 ${REPS:-2}); do
     echo "== $n (round $rep)"
     if [ -z "${NO_PRED}" ]; then
       DGPRF_LIB=$PWD/$lib timeout -k 10 120 python3 scripts/prof_predict.py --samples 20 || exit $?
+      DGPRF_LIB=$PWD/$lib timeout -k 10 120 python3 scripts/prof_predict.py --samples 20 --pairs || exit $?
     fi
     for c in ${CONFIGS:-2 4 5}; do
       DGPRF_LIB=$PWD/$lib timeout -k 10 200 python3 scripts/diag/step_graph.py $c 200 ${STEPS:-2000} || exit $?

@@ -9,7 +9,7 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 rc=$?
 tail -15 $O/pytest_gpu.log
 [ $rc -eq 0 ] || exit $rc
-NO_PRED=1 CONFIGS="${AB_CONFIGS:-2 4 5}" REPS=2 STEPS=2000 timeout -k 10 400 bash scripts/ab_variants.sh > $O/ab.log 2>&1 || { cat $O/ab.log; exit 5; }
+CONFIGS="${AB_CONFIGS:-2 4 5}" REPS=2 STEPS=2000 timeout -k 10 400 bash scripts/ab_variants.sh > $O/ab.log 2>&1 || { cat $O/ab.log; exit 5; }
 cat $O/ab.log
 timeout -k 10 300 python bench.py --steps 2000 --no-cpu-baseline --other-configs 0 --b-sweep 0 \
   --multi-chains 0 --full-bayes-steps 0 --eager-calls 0 > $O/bench.json 2> $O/bench.err || { tail $O/bench.err; exit 6; }

@@ -22,6 +22,7 @@ from models.regression_model import RegressionDGP  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--samples", type=int, default=10)
 ap.add_argument("--n-test", type=int, default=100_000)
+ap.add_argument("--pairs", action="store_true", help="two samples per pass (add_samples)")
 args = ap.parse_args()
 dev = torch.device("cuda", 0)
 _, _, a = regression_data(1000, 8, seed=0, device=dev)
@@ -30,12 +31,21 @@ E.set_seed(2)
 m = RegressionDGP(8, 1, n_hidden_layers=3, n_rf=1024, n_gp=[8, 8, 1], likelihood=Gaussian(variance=0.1))
 m.precond_update(None, 1_000_000, precond_type="identity")
 acc = PredictiveLSE(m._engine, Xt, Yt)
-acc.add_sample()
+th = torch.stack([m._engine.theta.clone(), m._engine.theta.clone()])
+if args.pairs:
+    th[1].mul_(0.5)
+    acc.add_samples(th)
+else:
+    acc.add_sample()
 ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 ev0.record()
-for _ in range(args.samples):
-    acc.add_sample(build=False)
+for _ in range(args.samples // (2 if args.pairs else 1)):
+    if args.pairs:
+        acc.add_samples(th, build=False)
+    else:
+        acc.add_sample(build=False)
 ev1.record()
 torch.cuda.synchronize()
-print(f"predictive: {ev0.elapsed_time(ev1) / args.samples * 1e3:.1f} us/sample; "
+k = args.samples // (2 if args.pairs else 1) * (2 if args.pairs else 1)
+print(f"predictive{' (pairs)' if args.pairs else ''}: {ev0.elapsed_time(ev1) / k * 1e3:.1f} us/sample; "
       f"finalize {acc.finalize()}")  # (the same numbers for every library build: a parity check)
