@@ -38,6 +38,13 @@ StepDev make_step_dev(const dgprf_plan_t& pl, const dgprf_chain_t& ch, const dgp
   sd.bd.perm_seed = b.perm_seed;
   sd.bd.y_cols = b.y_cols;
   sd.bd.mode = b.mode;
+  // resident A_1 rows (wide first layer, fixed Omega_1, a dataset to gather from); enqueue_step
+  // drops it for full-Bayes steps (Omega_1 changes in-step)
+  const bool res = b.A1 && pl.a0_off >= 0 && b.mode != DGPRF_BATCH_DIRECT && !(pl.fresh_z & 1) &&
+                   pl.n_rf[0] % 4 == 0;
+  sd.bd.A1 = res ? b.A1 : nullptr;
+  sd.bd.a1_ld = pl.n_rf[0];
+  sd.bd.pad = 0;
   sd.step_offset = step_offset;
   sd.full_bayes = 0;
   const bool pc = pl.hyp_per_chain != 0;
@@ -110,9 +117,11 @@ int check_step(const dgprf_step_t* st) {
 // step's minibatch rows first; gather_next: the update kernel gathers step t+1's rows (graph
 // replays, where the next step is known to follow).  The update kernel sums the gW partials and
 // updates every W (and the full-Bayes hyper-parameters).
-hipError_t enqueue_step(const dgprf_plan_t& pl, const StepDev& sd, const UpdateDev& ud,
+hipError_t enqueue_step(const dgprf_plan_t& pl, const StepDev& sd_in, const UpdateDev& ud,
                         hipStream_t s, bool prep_gather = true, bool gather_next = false) {
   hipError_t e = hipSuccess;
+  StepDev sd = sd_in;
+  if (sd.full_bayes) sd.bd.A1 = nullptr;  // Omega_1 changes every full-Bayes step: the GEMM
   if (prep_gather) e = dgprf::launch_gather(pl, sd, s);
   // random_fixed=False layers: this step's Omega from fresh z (layers/rf_layers.py:39-41)
   if (e == hipSuccess && pl.fresh_z) e = dgprf::launch_fresh_omega(pl, sd, s);
@@ -491,9 +500,9 @@ int dgprf_forward(const dgprf_plan_t* plan, const float* theta, const float* ome
 }
 
 int dgprf_forward_samples(const dgprf_plan_t* plan, const float* thetas, int32_t n_samples,
-                          const float* omega, const float* der, const float* X, const float* Y,
-                          int32_t y_cols, int64_t n, float* lse_m, float* lse_s, float* se_sum,
-                          float* scratch, int64_t scratch_floats, void* stream) {
+                          const float* omega, const float* der, const float* X, const float* A1,
+                          const float* Y, int32_t y_cols, int64_t n, float* lse_m, float* lse_s,
+                          float* se_sum, float* scratch, int64_t scratch_floats, void* stream) {
   int rc = check_plan(plan);
   if (rc) return rc;
   if (!thetas || n_samples < 1 || !omega || !der || n < 0 || (n > 0 && (!X || !Y)) || y_cols < 1 ||
@@ -503,9 +512,9 @@ int dgprf_forward_samples(const dgprf_plan_t* plan, const float* thetas, int32_t
   if (plan->likelihood == DGPRF_LIK_GAUSSIAN && y_cols < plan->n_gp[plan->n_layers - 1])
     return DGPRF_E_SHAPE;
   if (scratch_floats < 0 || (scratch_floats > 0 && !scratch)) return DGPRF_E_ARG;
-  if (scratch_floats < dgprf::forward_cfg(*plan, n).scratch_floats) return DGPRF_E_ARG;
-  return hip_rc(dgprf::launch_forward_samples(*plan, thetas, n_samples, omega, der, X, Y, y_cols, n,
-                                              lse_m, lse_s, se_sum, scratch, as_stream(stream)));
+  if (!A1 && scratch_floats < dgprf::forward_cfg(*plan, n).scratch_floats) return DGPRF_E_ARG;
+  return hip_rc(dgprf::launch_forward_samples(*plan, thetas, n_samples, omega, der, X, A1, Y, y_cols,
+                                              n, lse_m, lse_s, se_sum, scratch, as_stream(stream)));
 }
 
 int dgprf_lse_finalize(const float* lse_m, const float* lse_s, const float* se_sum, int32_t parts,

@@ -199,6 +199,8 @@ struct BatchDev {
   uint64_t perm_seed;
   int32_t y_cols;
   int32_t mode;
+  const float* A1;  // resident X Omega_1 [n_data][a1_ld] (wide first layer, fixed Omega_1) or null
+  int32_t a1_ld, pad;
 };
 
 __device__ __forceinline__ int64_t batch_row(const BatchDev& bd, int B, int chain, int64_t t,

@@ -1292,7 +1292,7 @@ hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const
                                const float* der, const float* X, const float* Y, int y_cols,
                                int64_t n, float* const* f_out, float* logp, float* se,
                                float* lse_m, float* lse_s, float* se_sum, float* scratch,
-                               hipStream_t s) {
+                               hipStream_t s, const float* a1_full) {
   if (n <= 0) return hipSuccess;
   FOut fo;
   for (int l = 0; l < DGPRF_MAX_LAYERS; ++l) fo.p[l] = (f_out && l < pl.n_layers) ? f_out[l] : nullptr;
@@ -1304,13 +1304,15 @@ hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const
   }
   const ForwardCfg cfg = forward_cfg(pl, n);
   const bool wide0 = cfg.wide0, tiles = cfg.tiles;
-  const int64_t chunk = cfg.chunk, R0 = pl.n_rf[0];
-  float* a0 = wide0 ? scratch : nullptr;
+  // a caller-resident A_1 of every row: one chunk, no GEMM
+  const bool res = wide0 && a1_full;
+  const int64_t chunk = res ? n : cfg.chunk, R0 = pl.n_rf[0];
+  float* a0 = res ? const_cast<float*>(a1_full) : (wide0 ? scratch : nullptr);
   if (wide0 && !a0) return hipErrorInvalidValue;
   hipError_t err = hipSuccess;
   for (int64_t r0 = 0; r0 < n && err == hipSuccess; r0 += chunk) {
     const int64_t r1 = std::min(n, r0 + chunk);
-    if (wide0) {
+    if (wide0 && !res) {
       err = launch_agemm(X + r0 * pl.d_in, r1 - r0, pl.d_in, pl.d[0], omega + pl.omega_off[0],
                          (int)R0, a0, s);
       if (err != hipSuccess) break;
@@ -1412,7 +1414,7 @@ bool forward_pairs_ok(const dgprf_plan_t& pl, int64_t n) {
 
 hipError_t launch_forward_samples(const dgprf_plan_t& pl, const float* thetas, int n_samples,
                                   const float* omega, const float* der, const float* X,
-                                  const float* Y, int y_cols, int64_t n, float* lse_m,
+                                  const float* A1, const float* Y, int y_cols, int64_t n, float* lse_m,
                                   float* lse_s, float* se_sum, float* scratch, hipStream_t s) {
   if (n <= 0 || n_samples <= 0) return hipSuccess;
   // 32-bit buffer offsets across two samples' W
@@ -1422,7 +1424,7 @@ hipError_t launch_forward_samples(const dgprf_plan_t& pl, const float* thetas, i
     for (int j = 0; j < n_samples; ++j) {
       const hipError_t e = launch_forward_rows(pl, thetas + (int64_t)j * pl.n_chains * pl.w_total,
                                                omega, der, X, Y, y_cols, n, nullptr, nullptr,
-                                               nullptr, lse_m, lse_s, se_sum, scratch, s);
+                                               nullptr, lse_m, lse_s, se_sum, scratch, s, A1);
       if (e != hipSuccess) return e;
     }
     return hipSuccess;

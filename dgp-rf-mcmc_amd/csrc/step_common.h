@@ -150,6 +150,8 @@ struct UpdK {
   BatchDev bd;
   float* xb;
   float* yb;
+  float* a0;  // resident A_1 rows of step t+1 (bd.A1): the workspace slab, chain 0
+  int32_t gather_blocks, a1_parts;
   // full_bayesian=True: the first hyp_blocks workgroups do the hyper-parameter work
   int32_t hyp_blocks, pad_h;
   HypK hk;
@@ -432,6 +434,30 @@ __device__ __forceinline__ void gather_row_wave(const BatchDev& bd, int B, int d
   for (int k = lane; k < yb_cols; k += 64) yb[(int64_t)b * yb_cols + k] = bd.Y[row * bd.y_cols + k];
 }
 
+// Resident first-layer projection (BatchDev.A1 = X Omega_1 of every dataset row): the 1,024-float
+// part `part` of minibatch row b's A_1 row into the workspace slab [align32(B)][R_1] the layer-0
+// kernels read — one wave, four 16-byte loads per lane issued before the stores.  Replaces the
+// step's A_1 = X_B Omega_1 GEMM (the rows of a product are the products of the rows).
+constexpr int A1_PART = 1024;
+__device__ __forceinline__ void gather_a1_part(const BatchDev& bd, int B, float* a0, int chain,
+                                               int64_t t, int b, int part, int lane) {
+  const int64_t row = batch_row(bd, B, chain, t, b);
+  const int R0 = bd.a1_ld;
+  const float* src = bd.A1 + row * R0;
+  float* dst = a0 + (int64_t)b * R0;
+  f4 v[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int k = part * A1_PART + 4 * (u * 64 + lane);
+    v[u] = k < R0 ? *reinterpret_cast<const f4*>(src + k) : f4zero();
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int k = part * A1_PART + 4 * (u * 64 + lane);
+    if (k < R0) *reinterpret_cast<f4*>(dst + k) = v[u];
+  }
+}
+
 // Schedule of step t (utils.py:49-73 via experiments/utils_training.py:41-61 when CYC).
 template <bool CYC>
 __device__ __forceinline__ void step_schedule(const UpdateDev& ud, int64_t t, float* lr, float* T,
@@ -625,7 +651,7 @@ inline LayerK make_layer_k(const dgprf_plan_t& pl, const StepDev& sd, int l, int
   if (sd.full_bayes) lds_floats += NW * round4(2 * a.d + 1);
   a.main_blocks = 8 * a.rt_per_xcd * a.ns;
   a.a0_sl = 0;
-  if (a.a0) {  // the A_1 GEMM's K parts (agemm.hip): two slabs, summed here as slab 0 + slab 1
+  if (a.a0 && !sd.bd.A1) {  // the A_1 GEMM's K parts (agemm.hip): two slabs, summed here as slab 0 + slab 1
     const int64_t rows = (pl.batch + 31) / 32 * 32;
     if (dgprf::agemm_parts(pl.batch, rows, pl.d_in, pl.d[0], pl.n_rf[0]) == 2)
       a.a0_sl = (int32_t)(rows * pl.n_rf[0]);

@@ -42,13 +42,22 @@ struct GatherK {
   const int64_t* step;
   float* xb;  // chain 0 (chain stride ws_cs)
   float* yb;
+  float* a0;  // resident A_1 rows (bd.A1): the workspace slab, chain 0
   int64_t ws_cs;
   int32_t B, d_in, yb_cols, step_offset;
+  int32_t row_blocks, a1_parts;
 };
 
 __global__ void k_gather(const GatherK a) {
   const int chain = blockIdx.y;
   const int64_t t = *a.step + a.step_offset;
+  if ((int)blockIdx.x >= a.row_blocks) {  // resident A_1: one wave per (row, part)
+    const int w = ((int)blockIdx.x - a.row_blocks) * (int)(blockDim.x >> 6) + (int)(threadIdx.x >> 6);
+    const int b = w / a.a1_parts, part = w - b * a.a1_parts;
+    if (b < a.B) gather_a1_part(a.bd, a.B, a.a0 + (int64_t)chain * a.ws_cs, chain, t, b, part,
+                                threadIdx.x & 63);
+    return;
+  }
   if (a.d_in > GATHER_WIDE) {  // one wave per row
     const int b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (b < a.B)
@@ -367,6 +376,14 @@ __global__ __launch_bounds__(UPD_THREADS) void k_step_update(const UpdK a) {
     return;
   }
   const int bx = (int)blockIdx.x - a.hyp_blocks;
+  if (bx >= a.upd_blocks + a.gather_blocks) {  // resident A_1 rows of step t+1: (row, part) each
+    const int64_t t = *a.step + (int64_t)a.step_offset;
+    const int w = bx - a.upd_blocks - a.gather_blocks;
+    const int b = w / a.a1_parts, part = w - b * a.a1_parts;
+    if (b < a.B) gather_a1_part(a.bd, a.B, a.a0 + (int64_t)chain * a.ws_cs, chain, t + 1, b, part,
+                                threadIdx.x);
+    return;
+  }
   if (bx >= a.upd_blocks) {  // dedicated blocks: rows of step t+1 (off the path)
     const int64_t t = *a.step + (int64_t)a.step_offset;
     if (a.d_in > GATHER_WIDE) {  // one-wave blocks: one row each
@@ -608,7 +625,9 @@ hipError_t launch_step_fwd(const dgprf_plan_t& pl, const StepDev& sd, int layer,
   const int nwf = (w8 && pl.cpw[layer] % 8 == 0) ? 16 : (w8 ? 8 : 4);
   int lds_floats = 0;
   LayerK a = make_layer_k(pl, sd, layer, lds_floats, false, nwf);
-  if (a.a0 && with_agemm) {  // wide first layer: A_1 = X Omega_1 first
+  // wide first layer: A_1 = X Omega_1 first — unless the rows were gathered from the dataset's
+  // resident projection (sd.bd.A1)
+  if (a.a0 && with_agemm && !sd.bd.A1) {
     const hipError_t e = launch_step_agemm(pl, sd, s);
     if (e != hipSuccess) return e;
   }
@@ -805,7 +824,12 @@ hipError_t launch_step_update(const dgprf_plan_t& pl, const StepDev& sd, const U
   }
   const int64_t gblocks = !a.gather_next ? 0 : (pl.d_in > GATHER_WIDE ? pl.batch
                                                     : (pl.batch + UPD_THREADS - 1) / UPD_THREADS);
-  const int64_t blocks = a.hyp_blocks + a.upd_blocks + gblocks;
+  a.gather_blocks = (int32_t)gblocks;
+  // resident A_1 rows of step t+1 (one-wave blocks, one per row and 1,024-float part)
+  a.a1_parts = (pl.n_rf[0] + A1_PART - 1) / A1_PART;
+  a.a0 = sd.ws && pl.a0_off >= 0 ? sd.ws + pl.a0_off : nullptr;
+  const int64_t ablocks = a.gather_next && sd.bd.A1 && a.a0 ? (int64_t)pl.batch * a.a1_parts : 0;
+  const int64_t blocks = a.hyp_blocks + a.upd_blocks + gblocks + ablocks;
   dim3 grid((unsigned)blocks, pl.n_chains);
   const bool xi = ud.xi != nullptr || ud.xi_resample != nullptr ||
                   (fb && (ud.xi_hyp != nullptr || ud.xi_hyp_resample != nullptr));
@@ -860,13 +884,18 @@ hipError_t launch_gather(const dgprf_plan_t& pl, const StepDev& sd, hipStream_t 
   a.step = sd.step;
   a.xb = sd.ws + pl.xb_off;
   a.yb = sd.ws + pl.yb_off;
+  a.a0 = pl.a0_off >= 0 ? sd.ws + pl.a0_off : nullptr;
   a.ws_cs = pl.ws_chain;
   a.B = pl.batch;
   a.d_in = pl.d_in;
   a.yb_cols = pl.yb_cols;
   a.step_offset = sd.step_offset;
   const int rows_per_block = pl.d_in > GATHER_WIDE ? 4 : 256;
-  dim3 grid((unsigned)((pl.batch + rows_per_block - 1) / rows_per_block), pl.n_chains);
+  a.row_blocks = (pl.batch + rows_per_block - 1) / rows_per_block;
+  a.a1_parts = (pl.n_rf[0] + A1_PART - 1) / A1_PART;
+  // resident A_1: 4 (row, part) waves per 256-thread block
+  const int ablocks = sd.bd.A1 && a.a0 ? (pl.batch * a.a1_parts + 3) / 4 : 0;
+  dim3 grid((unsigned)(a.row_blocks + ablocks), pl.n_chains);
   hipLaunchKernelGGL(k_gather, grid, dim3(256), 0, s, a);
   return hipGetLastError();
 }

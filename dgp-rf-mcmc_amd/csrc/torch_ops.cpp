@@ -63,7 +63,7 @@ dgprf_batch_t batch_of(const dgprf_plan_t& pl, const Tensor& X, const Tensor& Y,
   TORCH_CHECK(X.dim() == 2 && X.size(1) == pl.d_in, "dgprf: X must be [n, d_in]");
   TORCH_CHECK(Y.dim() == 2 && Y.size(0) == X.size(0), "dgprf: Y must be [n, y_cols]");
   dgprf_batch_t b;
-  std::memset(&b, 0, sizeof(b));
+  std::memset(&b, 0, sizeof(b));  // A1 = NULL: eager calls run the A_1 GEMM
   b.X = f32(X, "X");
   b.Y = f32(Y, "Y");
   b.n_data = X.size(0);
@@ -190,8 +190,9 @@ std::tuple<std::vector<Tensor>, Tensor, Tensor> forward(
 
 // thetas [S][C][w_total]: every sample of every chain folded into the LSE accumulators [C][n]
 void forward_samples(const Tensor& plan, const Tensor& thetas, const Tensor& omega,
-                     const Tensor& der, const Tensor& X, const Tensor& Y, const Tensor& lse_m,
-                     const Tensor& lse_s, const OptT& se_sum, const OptT& scratch) {
+                     const Tensor& der, const Tensor& X, const OptT& A1, const Tensor& Y,
+                     const Tensor& lse_m, const Tensor& lse_s, const OptT& se_sum,
+                     const OptT& scratch) {
   const dgprf_plan_t pl = plan_of(plan);
   const int64_t C = pl.n_chains, ch = pl.hyp_per_chain ? C : 1;
   TORCH_CHECK(X.dim() == 2 && X.size(1) == pl.d_in, "dgprf: X must be [n, d_in]");
@@ -200,13 +201,15 @@ void forward_samples(const Tensor& plan, const Tensor& thetas, const Tensor& ome
   TORCH_CHECK(thetas.dim() == 3 && thetas.size(1) == C && thetas.size(2) == pl.w_total,
               "dgprf: thetas must be [samples, n_chains, w_total]");
   const int64_t S = thetas.size(0);
+  // A1 rows past n up to a multiple of 64 are read (whole 64-row tile-kernel workgroups)
+  float* a1 = f32o(A1, "A1", (n + 63) / 64 * 64 * (int64_t)pl.n_rf[0]);
   int64_t need = 0;
   check_rc(dgprf_forward_scratch(&pl, n, &need), "dgprf_forward_scratch");
-  float* scr = f32o(scratch, "scratch", need);
-  TORCH_CHECK(need == 0 || scr, "dgprf: forward needs ", need, " floats of scratch");
+  float* scr = a1 ? nullptr : f32o(scratch, "scratch", need);
+  TORCH_CHECK(a1 || need == 0 || scr, "dgprf: forward needs ", need, " floats of scratch");
   check_rc(dgprf_forward_samples(&pl, f32(thetas, "thetas", S * C * pl.w_total), (int32_t)S,
                                  f32(omega, "omega", ch * pl.omega_total),
-                                 f32(der, "der", ch * pl.der_total), f32(X, "X"), f32(Y, "Y"),
+                                 f32(der, "der", ch * pl.der_total), f32(X, "X"), a1, f32(Y, "Y"),
                                  (int32_t)Y.size(1), n, f32(lse_m, "lse_m", C * n),
                                  f32(lse_s, "lse_s", C * n), f32o(se_sum, "se_sum", C * n), scr,
                                  scr ? scratch->numel() : 0, stream()),
@@ -248,8 +251,9 @@ TORCH_LIBRARY(dgprf, m) {
       "int f_mask, bool logp, bool se, Tensor(a!)? lse_m, Tensor(b!)? lse_s, Tensor(c!)? se_sum, "
       "Tensor(d!)? scratch) -> (Tensor[], Tensor, Tensor)");
   m.def(
-      "forward_samples(Tensor plan, Tensor thetas, Tensor omega, Tensor der, Tensor X, Tensor Y, "
-      "Tensor(a!) lse_m, Tensor(b!) lse_s, Tensor(c!)? se_sum, Tensor(d!)? scratch) -> ()");
+      "forward_samples(Tensor plan, Tensor thetas, Tensor omega, Tensor der, Tensor X, Tensor? A1, "
+      "Tensor Y, Tensor(a!) lse_m, Tensor(b!) lse_s, Tensor(c!)? se_sum, Tensor(d!)? scratch) "
+      "-> ()");
   m.def("lse_finalize(Tensor m, Tensor s, Tensor? e, float s_total, float y_std, bool lse_out) "
         "-> (Tensor, Tensor)");
 }

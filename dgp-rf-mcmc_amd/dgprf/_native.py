@@ -67,7 +67,7 @@ class Chain(ctypes.Structure):
 class Batch(ctypes.Structure):
     """dgprf_batch_t."""
     _fields_ = [("X", _vp), ("Y", _vp), ("idx", _vp), ("n_data", _i64), ("y_cols", _i32),
-                ("mode", _i32), ("iters_per_epoch", _i64), ("perm_seed", _u64)]
+                ("mode", _i32), ("iters_per_epoch", _i64), ("perm_seed", _u64), ("A1", _vp)]
 
 
 class Step(ctypes.Structure):
@@ -96,8 +96,8 @@ SIGNATURES = {
                                         ctypes.POINTER(Step), _i32]),
     "dgprf_graph_launch": (_i32, [_vp, _vp]),
     "dgprf_graph_destroy": (_i32, [_vp]),
-    "dgprf_forward_samples": (_i32, [ctypes.POINTER(Plan), _vp, _i32, _vp, _vp, _vp, _vp, _i32, _i64,
-                                     _vp, _vp, _vp, _vp, _i64, _vp]),
+    "dgprf_forward_samples": (_i32, [ctypes.POINTER(Plan), _vp, _i32, _vp, _vp, _vp, _vp, _vp, _i32,
+                                     _i64, _vp, _vp, _vp, _vp, _i64, _vp]),
     "dgprf_profile_step": (_i32, [ctypes.POINTER(Plan), ctypes.POINTER(Chain),
                                   ctypes.POINTER(Batch), ctypes.POINTER(Step), _i32, _vp, _vp]),
     "dgprf_forward_scratch": (_i32, [ctypes.POINTER(Plan), _i64, ctypes.POINTER(_i64)]),

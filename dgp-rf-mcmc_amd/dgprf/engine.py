@@ -121,6 +121,7 @@ class ModelSpec:
 
 class Engine:
     MAX_GRAPHS = 8  # instantiated step graphs kept per engine (LRU)
+    A1_MAX_BYTES = 8 << 30  # resident first-layer projections (dataset_a1) larger than this: GEMM
 
     def __init__(self, spec, n_chains=1, dev=None, seed=None, per_chain_hyp=None):
         """per_chain_hyp: every chain owns its kernel / likelihood hyper-parameters (and Omega),
@@ -155,6 +156,13 @@ class Engine:
         self._fwd_scratch = None
         self._plan_tensors = {}
         self.moments_ready = False
+        # wide first layer (d_1 > 32): X Omega_1 of a whole dataset / test set kept resident in HBM
+        # (dataset_a1), so steps gather their rows and predictive samples share it instead of
+        # running the A_1 GEMM; recomputed when Omega_1 may have changed (hyper_epoch counts device
+        # full-Bayes runs, whose hyper-parameter writes torch's version counters do not see)
+        self.resident_a1 = True
+        self.hyper_epoch = 0
+        self._a1_cache = {}
 
     # ---------------------------------------------------------------- views
     def W_view(self, l, chain=0):
@@ -368,6 +376,29 @@ class Engine:
         self.build_omega()
         return True
 
+    def dataset_a1(self, X):
+        """X Omega_1 for every row of X ([align64(n), n_rf[0]], rows past n zero), resident in HBM
+        and cached per (X, Omega_1 state) — the first-layer projection of the reference's
+        `tf.matmul(x, self.Omega)` (layers/rf_layers.py:42) for a wide first layer (d_1 > 32),
+        computed once by the hand-written MFMA GEMM (dgprf_rf_project) instead of per minibatch /
+        per posterior sample.  None when the layer is not wide, Omega_1 is per chain, or the
+        projection would exceed A1_MAX_BYTES.  Call after Omega is built."""
+        pl = self.layout
+        if pl.a0_off < 0 or not self.resident_a1 or (self.per_chain_hyp and self.C > 1):
+            return None
+        n, R0 = int(X.shape[0]), int(pl.n_rf[0])
+        rows = (n + 63) // 64 * 64
+        if rows * R0 * 4 > self.A1_MAX_BYTES or R0 % 4:
+            return None
+        key = (X.data_ptr(), tuple(X.shape))
+        okey = (X._version, self._omega_key(), self.hyper_epoch)
+        ent = self._a1_cache.get(key)
+        if ent is None or ent[1] != okey:
+            buf = ent[0] if ent is not None else torch.zeros(rows, R0, dtype=_F32, device=self.dev)
+            self.rf_project(X, self.omega_view(0), out=buf[:n])
+            self._a1_cache[key] = (buf, okey)
+        return self._a1_cache[key][0]
+
     # ---------------------------------------------------------------- hot path
     def _prep_batch(self, X, Y):
         X = as_device(X, self.dev)
@@ -423,6 +454,7 @@ class Engine:
         (models/dgp.py:199-216); Omega, c and sigma^2 are rebuilt on the device afterwards."""
         if full_bayes:
             self._check_full_bayes()
+            self.hyper_epoch += 1  # the device rewrites hyp / Omega: resident projections stale
         pl, ws, X, Y, idx, iters, ps = self._op_batch(X, Y, batch_size, mode, idx, perm_seed,
                                                       full_bayes)
         if build:
@@ -457,10 +489,15 @@ class Engine:
         fresh_z: layers (bit mask) whose z is redrawn every step (random_fixed=False)."""
         if full_bayes:
             self._check_full_bayes()
+            self.hyper_epoch += 1  # its replays rewrite hyp / Omega on the device
+        # W-only steps of a wide first layer with fixed z gather their rows of the dataset's
+        # resident X Omega_1 (graphs hold its pointer; refreshed in place here when stale, so a
+        # cached graph's rows follow the current Omega_1)
+        a1 = None if (full_bayes or (fresh_z & 1)) else self.dataset_a1(X_all)
         key = (X_all.data_ptr(), tuple(X_all.shape), Y_all.data_ptr(), tuple(Y_all.shape),
                int(batch_size), float(data_size), float(lr), float(beta), float(T),
                int(steps_per_graph), int(schedule), int(start_step), int(cycle_length),
-               bool(resample_head), int(perm_seed), bool(full_bayes), int(fresh_z))
+               bool(resample_head), int(perm_seed), bool(full_bayes), int(fresh_z), a1 is not None)
         if key in self._graphs:
             g = self._graphs.pop(key)  # most recently used last
             self._graphs[key] = g
@@ -475,12 +512,14 @@ class Engine:
         iters = X_all.shape[0] // int(batch_size)
         ch = self.chain_struct(ws)
         bt = self.batch_struct(X_all, Y_all, N.BATCH_EPOCH, iters=iters, perm_seed=perm_seed)
+        if a1 is not None:
+            bt.A1 = a1.data_ptr()
         st = self.step_struct(lr, beta, T, data_size, False, schedule, start_step, cycle_length,
                               resample_head, full_bayes=full_bayes)
         h = ctypes.c_void_p()
         N.call("dgprf_graph_create_sghmc", ctypes.byref(h), ctypes.byref(pl), ctypes.byref(ch),
                ctypes.byref(bt), ctypes.byref(st), int(steps_per_graph))
-        g = _Graph(h, (X_all, Y_all, ws), int(steps_per_graph))
+        g = _Graph(h, (X_all, Y_all, ws, a1), int(steps_per_graph))
         self._graphs[key] = g
         return g
 
@@ -540,10 +579,11 @@ class Engine:
             out["se"] = sq
         return out
 
-    def forward_samples(self, thetas, X, Y, lse, omega=None, build=True):
+    def forward_samples(self, thetas, X, Y, lse, omega=None, build=True, a1=None):
         """Fold S posterior samples of every chain (thetas [S, C, w_total]) into the LSE
         accumulators lse = (m, s, se_sum) [C, n] in sample order (dgprf::forward_samples): two
-        samples per pass with layer 0 shared where the model is lean (every layer d, g <= 8)."""
+        samples per pass with layer 0 shared where the model is lean (every layer d, g <= 8);
+        a1 = dataset_a1(X) for a wide first layer (no A_1 GEMM per sample)."""
         X = as_device(X, self.dev)
         Yd = as_device(Y, self.dev)
         if Yd.dim() == 1:
@@ -557,8 +597,8 @@ class Engine:
             self.build_omega()
         m, s, e = lse
         om = self.omega if omega is None else omega
-        ops().forward_samples(self._plan_t(self.layout), thetas, om, self.der, X, Yd, m, s, e,
-                              self.forward_scratch(X.shape[0]))
+        ops().forward_samples(self._plan_t(self.layout), thetas, om, self.der, X, a1, Yd, m, s, e,
+                              None if a1 is not None else self.forward_scratch(X.shape[0]))
 
     def forward_scratch(self, n):
         """Engine-owned scratch of dgprf_forward for n rows (the wide-first-layer A_1 chunks),

@@ -28,9 +28,23 @@ class PredictiveLSE:
             else None
         self.S = 0  # samples folded in (per rank, all chains)
 
+    def _a1(self, build, omega):
+        """The test set's resident X Omega_1 (wide first layer; shared by every sample, Omega_1
+        being fixed across samples), or None (the A_1 GEMM runs per sample)."""
+        if omega is not None:
+            return None
+        if build:
+            self.eng.build_omega()
+        return self.eng.dataset_a1(self.X)
+
     def add_sample(self, build=True, omega=None):
         """Score the engine's current theta (one sample per chain) on the test set."""
-        self.eng.forward(self.X, self.Y, lse=(self.m, self.s, self.e), build=build, omega=omega)
+        a1 = self._a1(build, omega)
+        if a1 is not None:
+            self.eng.forward_samples(self.eng.theta[None], self.X, self.Y, (self.m, self.s, self.e),
+                                     build=False, a1=a1)
+        else:
+            self.eng.forward(self.X, self.Y, lse=(self.m, self.s, self.e), build=build, omega=omega)
         self.S += self.eng.C
 
     def add_samples(self, thetas, build=True, omega=None):
@@ -40,8 +54,9 @@ class PredictiveLSE:
         thetas = E.as_device(thetas, self.eng.dev)
         if thetas.dim() == 2:
             thetas = thetas[:, None, :]
-        self.eng.forward_samples(thetas, self.X, self.Y, (self.m, self.s, self.e), build=build,
-                                 omega=omega)
+        a1 = self._a1(build, omega)
+        self.eng.forward_samples(thetas, self.X, self.Y, (self.m, self.s, self.e),
+                                 build=build and a1 is None, omega=omega, a1=a1)
         self.S += thetas.shape[0] * thetas.shape[1]
 
     def finalize(self, y_std=1.0, group=None):

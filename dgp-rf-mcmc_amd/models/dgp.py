@@ -449,6 +449,8 @@ class DGP_RF(Module):
                     if not self.BNN.layers[2 * l].random_fixed)
         if fresh and full_bayesian:
             raise NotImplementedError("run_sgmcmc with random_fixed=False needs full_bayesian=False")
+        if full_bayesian:
+            eng.hyper_epoch += 1  # these graphs rewrite hyp / Omega on the device
         X_all = E.as_device(X_all, eng.dev)
         Y_all = E.as_device(Y_all, eng.dev)
         if Y_all.dim() == 1:
@@ -459,7 +461,8 @@ class DGP_RF(Module):
                                  temperature, k, sched, start_step, cycle_length,
                                  resample_in_cycle_head, perm_seed, full_bayes=bool(full_bayesian),
                                  fresh_z=fresh)
-        # Omega, c, sigma^2 only when a hyper-parameter or z changed since the last build
+        # Omega, c, sigma^2 only when a hyper-parameter or z changed since the last build (and
+        # with them a wide first layer's resident dataset projection, before graphs capture it)
         eng.build_omega_if_stale()
         full, rest = divmod(int(n_steps), spg)
         plan = [(mk(spg), full)] if full else []

@@ -205,6 +205,13 @@ typedef struct dgprf_batch {
   int32_t mode;
   int64_t iters_per_epoch;  /* DGPRF_BATCH_EPOCH: floor(n_data / B) */
   uint64_t perm_seed;       /* DGPRF_BATCH_EPOCH */
+  const float *A1;          /* optional, wide first layer (plan.a0_off >= 0): X Omega_1 of every
+                               dataset row [n_data][n_rf[0]] (dgprf_rf_project of the whole
+                               dataset, kept resident in HBM).  W-only steps of an EPOCH / INDEXED
+                               batch then gather their minibatch's rows of it instead of running
+                               the A_1 GEMM every step (Omega_1 is fixed unless full_bayes or layer
+                               0 draws fresh z; both ignore A1).  The caller recomputes it whenever
+                               Omega_1 changes.  NULL: the GEMM.  ABI 8 */
 } dgprf_batch_t;
 
 /* One SGHMC/SGLD update's scalars: DGP_RF.sgmcmc_update(..., data_size, lr, momentum_decay,
@@ -325,9 +332,13 @@ int dgprf_forward(const dgprf_plan_t *plan, const float *theta, const float *ome
  * kernel) score two samples per pass with layer 0 computed once for the pair (Omega is fixed across
  * samples, layers/rf_layers.py:21-22); other models run one forward per sample.  ABI 8. */
 int dgprf_forward_samples(const dgprf_plan_t *plan, const float *thetas, int32_t n_samples,
-                          const float *omega, const float *der, const float *X, const float *Y,
-                          int32_t y_cols, int64_t n, float *lse_m, float *lse_s, float *se_sum,
-                          float *scratch, int64_t scratch_floats, void *stream);
+                          const float *omega, const float *der, const float *X, const float *A1,
+                          const float *Y, int32_t y_cols, int64_t n, float *lse_m, float *lse_s,
+                          float *se_sum, float *scratch, int64_t scratch_floats, void *stream);
+/* (A1: optional [align64(n)][n_rf[0]] = X Omega_1 for a wide first layer (plan.a0_off >= 0),
+ * computed once by dgprf_rf_project and shared by every sample — Omega_1 is fixed across samples
+ * — so no sample runs the A_1 GEMM; rows n .. align64(n) are read (whole 64-row workgroups) and
+ * their outputs discarded.  NULL: the GEMM per sample, in scratch chunks.) */
 int dgprf_lse_finalize(const float *lse_m, const float *lse_s, const float *se_sum,
                        int32_t parts, int64_t n, double s_total, float log_y_std, float y_std,
                        float *lse_out, double *out, void *stream);

@@ -223,12 +223,12 @@ int main() {
                       nullptr, nullptr, nullptr, 0, nullptr) == DGPRF_E_ARG);  // log p without Y
   CHECK(dgprf_forward(&ok, &f, &f, &f, &f, &f, 1, 10, nullptr, nullptr, nullptr, &f, nullptr,
                       nullptr, nullptr, 0, nullptr) == DGPRF_E_ARG);  // lse_m without lse_s
-  CHECK(dgprf_forward_samples(&ok, &f, 0, &f, &f, &f, &f, 1, 10, &f, &f, nullptr, nullptr, 0,
-                              nullptr) == DGPRF_E_ARG);
-  CHECK(dgprf_forward_samples(&ok, &f, 2, &f, &f, &f, &f, 1, 10, nullptr, &f, nullptr, nullptr, 0,
-                              nullptr) == DGPRF_E_ARG);
-  CHECK(dgprf_forward_samples(&ok, &f, 2, &f, &f, &f, &f, 1, 10, &f, &f, nullptr, nullptr, -1,
-                              nullptr) == DGPRF_E_ARG);
+  CHECK(dgprf_forward_samples(&ok, &f, 0, &f, &f, &f, nullptr, &f, 1, 10, &f, &f, nullptr,
+                              nullptr, 0, nullptr) == DGPRF_E_ARG);
+  CHECK(dgprf_forward_samples(&ok, &f, 2, &f, &f, &f, nullptr, &f, 1, 10, nullptr, &f, nullptr,
+                              nullptr, 0, nullptr) == DGPRF_E_ARG);
+  CHECK(dgprf_forward_samples(&ok, &f, 2, &f, &f, &f, nullptr, &f, 1, 10, &f, &f, nullptr,
+                              nullptr, -1, nullptr) == DGPRF_E_ARG);
   CHECK(dgprf_lse_finalize(&f, &f, nullptr, 0, 10, 1.0, 0.f, 1.f, nullptr, nullptr, nullptr) ==
         DGPRF_E_ARG);
   CHECK(dgprf_rf_omega(9, 1, 1, &f, &f, &f, &f, &f, &f, nullptr) == DGPRF_E_ARG);

@@ -268,6 +268,49 @@ def test_wide_first_layer_full_bayes_grad(dev):
     assert group_err([h[0], h[1]], [ref["log_amp"][0], ref["log_amp"][1]]) < 5e-4
 
 
+def test_resident_first_layer_projection_steps(dev):
+    """Wide first layer (d = 100 > 32), W-only graph steps: with Engine.resident_a1 the dataset's
+    X Omega_1 is computed once (dataset_a1, the 128x128 MFMA GEMM) and every step gathers its
+    minibatch's rows of it instead of running the step's A_1 GEMM; 6 graph steps match the GEMM
+    form to fp32 rounding (the two GEMMs sum K in different orders), replay deterministically, and
+    after an in-place hyper-parameter update (layer 0's length scales) the projection is rebuilt
+    so the two forms still agree."""
+    from dgprf import engine as E
+    from likelihoods import Softmax
+    from models.dgp import DGP_RF
+    mk = lambda: DGP_RF(100, 5, n_hidden_layers=2, n_rf=[256, 128], n_gp=[10, 5],
+                        likelihood=Softmax(), kernel_type_list=["RBF", "RBF"])
+    models = []
+    for _ in range(3):
+        E.set_seed(54)
+        models.append(mk())
+    a, b, c = models
+    b._engine.resident_a1 = False
+    n = 2000
+    X = torch.rand(n, 100, device=dev) * 2 - 1
+    Y = torch.randint(0, 5, (n, 1), device=dev).float()
+    for mm in models:
+        mm.precond_update(None, n, precond_type="identity")
+    for mm in (b, c):
+        mm._engine.mom.copy_(a._engine.mom)
+    run = dict(batch_size=96, lr=0.02, momentum_decay=0.9, steps_per_graph=3, perm_seed=2)
+    for rnd in range(2):
+        for mm in models:
+            mm.run_sgmcmc(X, Y, n, 6, **run)
+        torch.cuda.synchronize()
+        assert a._engine._a1_cache and not b._engine._a1_cache
+        scale = float(b._engine.theta.abs().max())
+        assert float((a._engine.theta - b._engine.theta).abs().max()) <= 2e-5 * scale, rnd
+        assert torch.equal(a._engine.theta, c._engine.theta), rnd  # deterministic replays
+        with torch.no_grad():  # MCEM-style in-place update: Omega_1 and the projection rebuild
+            for mm in models:
+                mm.kernel_list[0].log_inv_length_scale.sub_(0.1)
+    buf = next(iter(a._engine._a1_cache.values()))[0]
+    ref = X.double() @ a._engine.omega_view(0).double()
+    assert float((buf[:n].double() - ref).abs().max()) <= 2e-5 * float(ref.abs().max())
+    assert torch.all(buf[n:] == 0)
+
+
 def test_wide_first_layer_two_chains_two_k_parts(dev):
     """C = 2 chains with a wide first layer (d = 100 > 32) at B = 96: the step's A_1 GEMM in two K
     parts (agemm.hip: blockIdx.y = chain x 2 + part, per-chain slab strides) feeding the layer-0
