@@ -32,6 +32,8 @@ for B in batches:
     m = DGP_RF(c["d_in"], c["d_out"], n_hidden_layers=len(c["kinds"]), n_rf=c["n_rf"],
                n_gp=c["n_gp"], likelihood=lik, kernel_type_list=c["kinds"])
     m.precond_update(None, c["n"], precond_type="identity")
+    if os.environ.get("DGPRF_DIAG_NO_A1"):  # per-step A_1 GEMM instead of the resident projection
+        m._engine.resident_a1 = False
     if os.environ.get("DGPRF_DIAG_FWD"):  # forward path of the fused step forward (diagnostic)
         from dgprf import _native as N
         m._engine.set_forward_path(getattr(N, "FWD_" + os.environ["DGPRF_DIAG_FWD"].upper()))
