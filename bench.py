@@ -262,6 +262,11 @@ def bench_config(cfg, dev, rank, world, barrier_sync, max_over_ranks, steps):
     t_p = max_over_ranks(time.perf_counter() - t0)
     k_ms = ev0.elapsed_time(ev1) / S
     fp = pred_flops(nt, d, R, P, g)
+    # a wide first layer's X_test Omega_1 is computed once and shared by every sample (resident
+    # projection): executed FLOPs per sample exclude it
+    pred_a1_shared = pl.a0_off >= 0 and m._engine.dataset_a1(Xt) is not None
+    if pred_a1_shared:
+        fp -= 2 * nt * d[0] * R[0]
     out = {"workload": f"{L}-layer {'/'.join(c['kinds'])} n_rf={c['n_rf'][0]} g={c['n_gp']} "
                        f"D={c['d_in']} N={n} B={c['batch']} {c['likelihood']}",
            "steps_per_s": round(world * steps / t_s, 1),
@@ -278,6 +283,9 @@ def bench_config(cfg, dev, rank, world, barrier_sync, max_over_ranks, steps):
            "test_loglik": round(ll, 5),
            "predictive_kernel_ms": round(k_ms, 3),
            "predictive_mfma_frac": round(fp / (k_ms * 1e-3) / FP32_MFMA_PEAK, 4),
+           "predictive_flops_per_sample": int(fp),
+           "predictive_a1": ("X_test Omega_1 resident, shared by every sample (not counted)"
+                             if pred_a1_shared else None),
            "a1_gemm": a1}
     del m, acc, X, Y, Xt, Yt
     torch.cuda.empty_cache()
