@@ -29,4 +29,5 @@ python3 $R/scripts/pmc_traffic_json.py $P > /dev/null || exit 2
 cp $P/* $O/
 cd $R
 timeout -k 10 500 python3 bench.py ${BENCH_ARGS} > $O/bench_plain.json 2> $O/bench_plain.err || exit $?
+cp $O/bench_plain.json $P/bench_plain.json
 tail -c 600 $O/bench_plain.json
