@@ -320,10 +320,6 @@ int dgprf_forward(const dgprf_plan_t *plan, const float *theta, const float *ome
                   float *const *f_out, float *logp, float *se, float *lse_m, float *lse_s,
                   float *se_sum, float *scratch, int64_t scratch_floats, void *stream);
 
-/* Posterior-predictive summary (experiments/utils_training.py:79-85):
- * per point lse[n] = log sum_s exp(lp_s) over all chains' accumulators, and
- * out[0] = mean_n(lse - log S_total) - log_y_std, out[1] = sqrt(sum se / (S_total n)) * y_std.
- * lse_m/lse_s/se_sum are [parts][n] (chains x ranks), combined in fixed order. */
 /* Posterior-predictive fold of several posterior samples of every chain (the driver's loop over W
  * samples, experiments/utils_training.py:79-85): thetas [n_samples][n_chains][w_total]; each
  * sample's per-row log p (and squared error) is folded into the chain's online log-sum-exp
@@ -339,6 +335,10 @@ int dgprf_forward_samples(const dgprf_plan_t *plan, const float *thetas, int32_t
  * computed once by dgprf_rf_project and shared by every sample — Omega_1 is fixed across samples
  * — so no sample runs the A_1 GEMM; rows n .. align64(n) are read (whole 64-row workgroups) and
  * their outputs discarded.  NULL: the GEMM per sample, in scratch chunks.) */
+/* Posterior-predictive summary (experiments/utils_training.py:79-85):
+ * per point lse[n] = log sum_s exp(lp_s) over all chains' accumulators, and
+ * out[0] = mean_n(lse - log S_total) - log_y_std, out[1] = sqrt(sum se / (S_total n)) * y_std.
+ * lse_m/lse_s/se_sum are [parts][n] (chains x ranks), combined in fixed order. */
 int dgprf_lse_finalize(const float *lse_m, const float *lse_s, const float *se_sum,
                        int32_t parts, int64_t n, double s_total, float log_y_std, float y_std,
                        float *lse_out, double *out, void *stream);
