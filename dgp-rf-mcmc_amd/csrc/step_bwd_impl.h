@@ -34,8 +34,11 @@ __device__ __forceinline__ void stage_slice_lds(const LayerK& a, const float* W,
 }
 
 
-// NWB: waves per workgroup (8: W-only, whole-slice LDS image).
-template <int KS, int NOT, bool RBF, bool G1, bool FB, int NWB>
+// NWB: waves per workgroup (8: W-only, whole-slice LDS image).  GSM: how the gW partial tile
+// leaves (1 < g): 0 = chosen at run time (g % 16 == 0: transposed tile, 16-byte lanes; else dword
+// stores from the MFMA tile), 1 = transposed tile only, 2 = staged per wave in LDS and stored as
+// contiguous 16-byte lanes only (a.gst_off).
+template <int KS, int NOT, bool RBF, bool G1, bool FB, int NWB, int GSM>
 __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT == 1 && !FB && (KS == 1 || KS == 2 || (KS == 4 && !RBF))) ? STEP_WPE : 1))) void k_step_bwd(const LayerK a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr bool WST = NWB == 8;  // whole-slice staging (a.wstage == 1 exactly then)
@@ -59,6 +62,8 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
   const int nit = cpw * 4 / NWB;
   constexpr int KGM = 4 * NOT;  // k-steps of the dPhi contraction (K = g)
   const int ND = (dxw + 15) >> 4;
+  // dX tiles held per lane: dxw = g_{l-1} <= d_l, so at most ceil(4 KS / 16) of them (KS > 0)
+  constexpr int NDM = KS == 0 ? 4 : (KS + 3) / 4;
   // dPhi / dA are needed for dX (l > 0) and, with full_bayesian=True, for every layer
   const bool dphi = FB || dxw > 0;
 
@@ -242,7 +247,10 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
   const rsrc_t rgw = make_rsrc(a.gwp + (int64_t)chain * a.ws_cs + (int64_t)rt * a.w_cs, a.w_cs);
   auto gw_store = [&](int64_t i, float v) { bstore1_wt(v, rgw, (uint32_t)(i * 4)); };
   auto gw_store4 = [&](int64_t i, f4 v) { bstore4_wt(v, rgw, (uint32_t)(i * 4)); };  // i % 4 == 0
-  f4 dxa[4] = {f4zero(), f4zero(), f4zero(), f4zero()};
+  float* gst = smem + a.gst_off + wave * 2 * 16 * g;  // this wave's gW tile staging (g % 16 != 0)
+  f4 dxa[NDM];
+#pragma unroll
+  for (int dt = 0; dt < NDM; ++dt) dxa[dt] = f4zero();
   // full_bayesian=True: per-wave sums over this row tile and the wave's features of
   //   hw[k]     = sum_b X[b][k] (dA z^T)[b][k]   (-> log_inv_ls)
   //   hw[d + k] = sum_b X[b][k] rowsum(dA)[b]    (-> mean)
@@ -272,7 +280,7 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
     //   at_n: features in registers (dA -> dX = dA Omega^T, K = features)
     //   dPhi = dF W^T in the features-in-registers orientation (K = g)
     float wd0[KGM], wd1[KGM];
-    f4 oxv[4];
+    f4 oxv[NDM];
     // this chunk's 64-feature block: the per-chunk staging buffers, or its rows of the slice image
     const float* wsc = WST ? smem + a.wsa_off + i * NWB * 16 * g : wsl;
     const int whalf = WST ? 64 * cpw * g : nwh;
@@ -289,7 +297,7 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
       }
       // rows k >= dxw of the staged block are never written: they only feed discarded outputs
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt)
+      for (int dt = 0; dt < NDM; ++dt)
         oxv[dt] = *reinterpret_cast<const f4*>(osc + (dt * 16 + lr) * ostc + wave * 16 + 4 * lq);
     }
     // layer 0 with d > 32: both orientations read the precomputed A_1 (k_step_agemm)
@@ -370,7 +378,8 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
       // written 16 bytes per lane (config 5 94.1 -> 93.0 us/step); other widths keep gW's own
       // orientation and dword stores (16- / 8-byte stores measured slower there: config 2 27.0 ->
       // 27.4, config 4 108.6 -> 121.8 us/step)
-      const bool t16 = (g & 15) == 0;
+      const bool t16 = GSM == 1 || (GSM == 0 && (g & 15) == 0);
+      constexpr bool gsv = GSM == 2;
 #pragma unroll
       for (int ot = 0; ot < NOT; ++ot) {
         f4 gc = f4zero(), gs = f4zero();
@@ -392,13 +401,16 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
             gc = mfma16(q0[r], dfg[ot][r], gc);
             if (RBF) gs = mfma16(q1[r], dfg[ot][r], gs);
           }
-          // gc[r] = gW[f0 + 4lq + r][ot*16 + lr]
+          // gc[r] = gW[f0 + 4lq + r][ot*16 + lr]: to the wave's LDS tile [2][16][g], or stored
           const int o = ot * 16 + lr;
           if (o < g) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const int f = f0 + 4 * lq + r;
-              if (f < R) {
+              if (gsv) {
+                gst[(4 * lq + r) * g + o] = gc[r];
+                if (RBF) gst[(16 + 4 * lq + r) * g + o] = gs[r];
+              } else if (GSM == 0 && f < R) {
                 gw_store((int64_t)f * g + o, gc[r]);
                 if (RBF) gw_store((int64_t)(R + f) * g + o, gs[r]);
               }
@@ -407,11 +419,31 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
         }
         DGPRF_STAMP(stamp_base, 9);
       }
+      if (gsv) {
+        // rows f0 .. f0 + 15 of gW (and of its sin half) are one contiguous run of 16 g floats,
+        // written as float4 lanes when every run starts 16-byte aligned (f0 g is a multiple of 16;
+        // the sin half starts R g floats on); rows past R are not stored
+        __builtin_amdgcn_wave_barrier();
+        const int nfl = min(16, R - f0) * g;
+        const bool v4 = ((R * g) & 3) == 0 && (nfl & 3) == 0;
+#pragma unroll
+        for (int h = 0; h < (RBF ? 2 : 1); ++h) {
+          const int64_t gb = (int64_t)(h * R + f0) * g;
+          const float* src = gst + h * 16 * g;
+          if (v4) {
+            for (int j = lane; 4 * j < nfl; j += 64)
+              gw_store4(gb + 4 * j, *reinterpret_cast<const f4*>(src + 4 * j));
+          } else {
+            for (int j = lane; j < nfl; j += 64) gw_store(gb + j, src[j]);
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
     }
     DGPRF_STAMP(stamp_base, 6);
     if (dxw > 0) {
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt)
+      for (int dt = 0; dt < NDM; ++dt)
         if (dt < ND) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) dxa[dt] = mfma16(oxv[dt][r], da[r], dxa[dt]);
@@ -471,7 +503,7 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
     const int DPS = ND * 16 + 4;
     float* redw = red + wave * TR * DPS;
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
+    for (int dt = 0; dt < NDM; ++dt)
       if (dt < ND) *reinterpret_cast<f4*>(redw + lr * DPS + dt * 16 + 4 * lq) = dxa[dt];
     __syncthreads();
     float* dxp = a.dxout + (int64_t)chain * a.ws_cs + (int64_t)sl * B * dxw;
@@ -492,22 +524,28 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
 }
 
 // backward: KS x NOT x RBF x G1 x FB x waves per workgroup (8: W-only with whole-slice staging)
+// the 8-wave (whole-slice) instances fix the gW store form at compile time: transposed tile for
+// g % 16 == 0 (and g == 1, which uses neither), LDS-staged otherwise (make_layer_k reserves the
+// staging whenever it keeps the whole-slice layout)
 template <int KS, int NOT, bool G1>
-void k_step_bwd_launch3(bool rbf, bool fb, bool w8, dim3 grid, size_t lds, hipStream_t s,
-                        const LayerK& a) {
-#define DGPRF_BWD(R_, F_, W_)                                                                 \
-  do {                                                                                       \
-    dgprf::set_lds_limit((const void*)k_step_bwd<KS, NOT, R_, G1, F_, W_>, lds);            \
-    hipLaunchKernelGGL((k_step_bwd<KS, NOT, R_, G1, F_, W_>), grid, dim3(64 * W_), lds, s, a); \
+void k_step_bwd_launch3(bool rbf, bool fb, bool w8, bool t16, dim3 grid, size_t lds,
+                        hipStream_t s, const LayerK& a) {
+#define DGPRF_BWD(R_, F_, W_, M_)                                                                  \
+  do {                                                                                            \
+    dgprf::set_lds_limit((const void*)k_step_bwd<KS, NOT, R_, G1, F_, W_, M_>, lds);             \
+    hipLaunchKernelGGL((k_step_bwd<KS, NOT, R_, G1, F_, W_, M_>), grid, dim3(64 * W_), lds, s, a); \
   } while (0)
+  constexpr int GS = G1 ? 1 : 2;
   if (rbf) {
-    if (fb) DGPRF_BWD(true, true, 4);
-    else if (w8) DGPRF_BWD(true, false, 8);
-    else DGPRF_BWD(true, false, 4);
+    if (fb) DGPRF_BWD(true, true, 4, 0);
+    else if (w8 && t16) DGPRF_BWD(true, false, 8, 1);
+    else if (w8) DGPRF_BWD(true, false, 8, GS);
+    else DGPRF_BWD(true, false, 4, 0);
   } else {
-    if (fb) DGPRF_BWD(false, true, 4);
-    else if (w8) DGPRF_BWD(false, false, 8);
-    else DGPRF_BWD(false, false, 4);
+    if (fb) DGPRF_BWD(false, true, 4, 0);
+    else if (w8 && t16) DGPRF_BWD(false, false, 8, 1);
+    else if (w8) DGPRF_BWD(false, false, 8, GS);
+    else DGPRF_BWD(false, false, 4, 0);
   }
 #undef DGPRF_BWD
 }
@@ -515,11 +553,12 @@ template <int KS>
 void k_step_bwd_launch2(int g, bool rbf, bool fb, bool w8, dim3 grid, size_t lds, hipStream_t s,
                         const LayerK& a) {
   const int NOT = (g + 15) >> 4;
-  if (g == 1) k_step_bwd_launch3<KS, 1, true>(rbf, fb, w8, grid, lds, s, a);
-  else if (NOT == 1) k_step_bwd_launch3<KS, 1, false>(rbf, fb, w8, grid, lds, s, a);
-  else if (NOT == 2) k_step_bwd_launch3<KS, 2, false>(rbf, fb, w8, grid, lds, s, a);
-  else if (NOT == 3) k_step_bwd_launch3<KS, 3, false>(rbf, fb, w8, grid, lds, s, a);
-  else k_step_bwd_launch3<KS, 4, false>(rbf, fb, w8, grid, lds, s, a);
+  const bool t16 = (g & 15) == 0;
+  if (g == 1) k_step_bwd_launch3<KS, 1, true>(rbf, fb, w8, t16, grid, lds, s, a);
+  else if (NOT == 1) k_step_bwd_launch3<KS, 1, false>(rbf, fb, w8, t16, grid, lds, s, a);
+  else if (NOT == 2) k_step_bwd_launch3<KS, 2, false>(rbf, fb, w8, t16, grid, lds, s, a);
+  else if (NOT == 3) k_step_bwd_launch3<KS, 3, false>(rbf, fb, w8, t16, grid, lds, s, a);
+  else k_step_bwd_launch3<KS, 4, false>(rbf, fb, w8, t16, grid, lds, s, a);
 }
 
 }  // namespace dgprf_sk

@@ -75,7 +75,9 @@ struct LayerK {
   // whole-slice staging (backward, cpw >= 4): the workgroup's W rows [h][64 cpw][g] and Omega rows
   // [dxw][64 cpw + 4] are copied global -> LDS once (global_load_lds) instead of one 64-feature
   // block per chunk with a load round trip and two barriers each
-  int32_t wstage, wsa_off, osa_off, osa_st, kind_rbf, pad_w;
+  int32_t wstage, wsa_off, osa_off, osa_st, kind_rbf;
+  // per-tile backward, 1 < g with g % 16 != 0: per-wave gW staging [nwb][2][16][g] (0: none)
+  int32_t gst_off;
   int32_t main_blocks;  // this layer's (row tile, slice) workgroups
   int32_t a0_sl;  // layer 0 with a0: second K-part slab of A_1 at a0 + a0_sl (0: one slab)
   // row-group backward (k_step_bwd_rg, minibatches of > 16 row tiles): rt_per_rg row tiles per
@@ -631,7 +633,6 @@ inline LayerK make_layer_k(const dgprf_plan_t& pl, const StepDev& sd, int l, int
   a.lik_fb = (pl.hyp_flags & DGPRF_HYP_LIK) != 0 && pl.likelihood == DGPRF_LIK_GAUSSIAN;
   // whole-slice staging for the backward (used only where dPhi / dX need W and Omega)
   a.kind_rbf = pl.kind[l] == DGPRF_RBF;
-  a.pad_w = 0;
   a.wstage = 0;
   a.wsa_off = a.osa_off = a.osa_st = 0;
   {
@@ -649,6 +650,20 @@ inline LayerK make_layer_k(const dgprf_plan_t& pl, const StepDev& sd, int l, int
   }
   a.hred_off = lds_floats;
   if (sd.full_bayes) lds_floats += NW * round4(2 * a.d + 1);
+  // whole-slice (8-wave) backward, gW partial tiles of widths that are not a multiple of 16: they
+  // leave the MFMA as 16-float row pieces (64 / 56 / 32 B at a row stride of g floats), so they are
+  // staged per wave in LDS and the wave's 16 feature rows (contiguous in W) go out as whole 16-byte
+  // lanes (config 4, g = 30 / 10).  The 4-wave instances keep dword stores: the staging put the
+  // config-2 backward (168-VGPR budget) over its registers.
+  a.gst_off = 0;
+  if (a.wstage && a.g > 1 && (a.g & 15) != 0) {
+    if (round4(lds_floats) + nwb * 2 * 16 * a.g <= 40 * 1024) {
+      a.gst_off = round4(lds_floats);
+      lds_floats = a.gst_off + nwb * 2 * 16 * a.g;
+    } else {
+      a.wstage = 0;  // no room for the staging next to the slice image: the 4-wave form
+    }
+  }
   a.main_blocks = 8 * a.rt_per_xcd * a.ns;
   a.a0_sl = 0;
   if (a.a0 && !sd.bd.A1) {  // the A_1 GEMM's K parts (agemm.hip): two slabs, summed here as slab 0 + slab 1
