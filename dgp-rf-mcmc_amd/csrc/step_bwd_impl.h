@@ -50,7 +50,7 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
   const int R = a.R, g = a.g, d = a.d, B = a.B, cpw = a.cpw, dxw = a.dxw;
   const int row0 = rt * TR;
   const int stamp_base = (a.layer * 2 + 1) * 4096 + blockIdx.z * gridDim.x + blockIdx.x;
-  DGPRF_STAMP(stamp_base, 0);
+  STEP_STAMP(stamp_base, 0);
   float* xs = smem;
   float* dfs = smem + a.aux_off;
   const int dfst = a.auxst;
@@ -142,14 +142,14 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
       const int k = threadIdx.x >> 4, c4 = threadIdx.x & 15;
       so = bload4(ro, k < dxw && fb0 + 4 * c4 < R ? (uint32_t)((k * R + fb0 + 4 * c4) * 4) : DGPRF_OOB);
     }
-    DGPRF_STAMP(stamp_base, 1);
+    STEP_STAMP(stamp_base, 1);
     elem_prologue(a, chain, row0, TR * g, xs, dfs, dfst, ysh, red);
     if (!WST && dphi) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) *reinterpret_cast<f4*>(wsl + 4 * ((int)threadIdx.x + 256 * j)) = sw[j];
       *reinterpret_cast<f4*>(osl + (threadIdx.x >> 4) * OST + 4 * (threadIdx.x & 15)) = so;
     }
-    DGPRF_STAMP(stamp_base, 4);
+    STEP_STAMP(stamp_base, 4);
   } else {
     if (WST && dphi) stage_slice_lds(a, W, om, fb0, smem);
     if (!WST && dphi) stage_load(fb0);
@@ -213,7 +213,7 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
   }
   if (!WST && !a.fast && dphi) stage_store(fb0);
   __syncthreads();
-  DGPRF_STAMP(stamp_base, 2);
+  STEP_STAMP(stamp_base, 2);
 
   float xf[8];
 #pragma unroll
@@ -351,7 +351,7 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
         }
       }
     }
-    DGPRF_STAMP(stamp_base, 8);
+    STEP_STAMP(stamp_base, 8);
     // ---- phase 3: gW_l partial of this row tile, then dX
     if (G1) {
       // g == 1: gW[f] = sum_b Phi[b][f] dF[b]: 4 rows per lane, then across the 4 row groups
@@ -417,7 +417,7 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
             }
           }
         }
-        DGPRF_STAMP(stamp_base, 9);
+        STEP_STAMP(stamp_base, 9);
       }
       if (gsv) {
         // rows f0 .. f0 + 15 of gW (and of its sin half) are one contiguous run of 16 g floats,
@@ -431,8 +431,11 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
           const int64_t gb = (int64_t)(h * R + f0) * g;
           const float* src = gst + h * 16 * g;
           if (v4) {
-            for (int j = lane; 4 * j < nfl; j += 64)
-              gw_store4(gb + 4 * j, *reinterpret_cast<const f4*>(src + 4 * j));
+#pragma unroll
+            for (int it = 0; it < NOT; ++it) {  // 16 g <= 256 NOT floats: NOT passes of 64 lanes
+              const int j = lane + 64 * it;
+              if (4 * j < nfl) gw_store4(gb + 4 * j, *reinterpret_cast<const f4*>(src + 4 * j));
+            }
           } else {
             for (int j = lane; j < nfl; j += 64) gw_store(gb + j, src[j]);
           }
@@ -440,7 +443,7 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
         __builtin_amdgcn_wave_barrier();
       }
     }
-    DGPRF_STAMP(stamp_base, 6);
+    STEP_STAMP(stamp_base, 6);
     if (dxw > 0) {
 #pragma unroll
       for (int dt = 0; dt < NDM; ++dt)
@@ -484,7 +487,7 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
       }
     }
   }
-  DGPRF_STAMP(stamp_base, 3);
+  STEP_STAMP(stamp_base, 3);
   if (FB) {
     // log_amp term over the wave, then the workgroup's partial row [2d+1] in wave order
     float v = sum16(ampl);
@@ -520,7 +523,7 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
 #ifdef DGPRF_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
-  DGPRF_STAMP(stamp_base, 14);
+  STEP_STAMP(stamp_base, 14);
 }
 
 // backward: KS x NOT x RBF x G1 x FB x waves per workgroup (8: W-only with whole-slice staging)

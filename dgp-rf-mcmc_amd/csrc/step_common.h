@@ -42,6 +42,26 @@ constexpr int OST = 68;  // LDS row stride of the staged Omega block (16B-aligne
 
 __host__ __device__ __forceinline__ int round4(int x) { return (x + 3) & ~3; }
 
+// In-kernel timestamps of the per-tile step kernels, diagnostic -DDGPRF_STAMPS build only: into the
+// buffer the launcher passes in a.stamps (16 slots per base; 15 / 13 = real time at slots 0 / 14).
+#ifdef DGPRF_STAMPS
+#define STEP_STAMP(base, i)                                                              \
+  do {                                                                                   \
+    if (threadIdx.x == 0 && a.stamps && (size_t)(base) < (size_t)17 * 4096) {             \
+      __builtin_amdgcn_sched_barrier(0);                                                 \
+      a.stamps[(size_t)(base) * 16 + (i)] = __builtin_amdgcn_s_memtime();                \
+      if ((i) == 0) a.stamps[(size_t)(base) * 16 + 15] = __builtin_amdgcn_s_memrealtime(); \
+      if ((i) == 14) a.stamps[(size_t)(base) * 16 + 13] = __builtin_amdgcn_s_memrealtime(); \
+      __builtin_amdgcn_sched_barrier(0);                                                 \
+    }                                                                                    \
+  } while (0)
+#else
+#define STEP_STAMP(base, i) \
+  do {                      \
+    (void)(base);           \
+  } while (0)
+#endif
+
 // Arguments of one forward / backward launch of layer `layer` (host-precomputed).
 struct LayerK {
   const float* om;      // Omega_l [d][R] of chain 0 (chain stride om_cs; 0 = shared)
@@ -653,8 +673,8 @@ inline LayerK make_layer_k(const dgprf_plan_t& pl, const StepDev& sd, int l, int
   // whole-slice (8-wave) backward, gW partial tiles of widths that are not a multiple of 16: they
   // leave the MFMA as 16-float row pieces (64 / 56 / 32 B at a row stride of g floats), so they are
   // staged per wave in LDS and the wave's 16 feature rows (contiguous in W) go out as whole 16-byte
-  // lanes (config 4, g = 30 / 10).  The 4-wave instances keep dword stores: the staging put the
-  // config-2 backward (168-VGPR budget) over its registers.
+  // lanes (config 4, g = 30 / 10).  The 4-wave instances keep dword stores: the staging puts the
+  // config-2 backward (168-VGPR budget) 15 VGPRs over (4 spilled without it).
   a.gst_off = 0;
   if (a.wstage && a.g > 1 && (a.g & 15) != 0) {
     if (round4(lds_floats) + nwb * 2 * 16 * a.g <= 40 * 1024) {

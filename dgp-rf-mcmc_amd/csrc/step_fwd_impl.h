@@ -17,7 +17,7 @@ __global__ __launch_bounds__(64 * NWB) void k_step_fwd(const LayerK a) {
   const int R = a.R, g = a.g, d = a.d, B = a.B, cpw = a.cpw;
   const int row0 = rt * TR;
   const int stamp_base = (a.layer * 2) * 4096 + blockIdx.z * gridDim.x + blockIdx.x;
-  DGPRF_STAMP(stamp_base, 0);
+  STEP_STAMP(stamp_base, 0);
   float* xs = smem;
   float* red = smem + a.red_off;
   const float* __restrict__ W = a.W + (int64_t)chain * a.w_cs;
@@ -30,7 +30,7 @@ __global__ __launch_bounds__(64 * NWB) void k_step_fwd(const LayerK a) {
   if (KS > 0) load_om_frag<KS>(om, R, d, chunk_f0(0), lr, lq, omk);
   load_w_frag<NOT, RBF, G1>(W, R, g, chunk_f0(0), lr, lq, wf);
   const float cl = a.cptr[(int64_t)chain * a.der_cs];
-  DGPRF_STAMP(stamp_base, 1);
+  STEP_STAMP(stamp_base, 1);
   if (a.fast) {
     elem_prologue(a, chain, row0, 0, xs, red, 0, red, red);  // no dF tile: unused targets
   } else if (KS > 0 || !a.a0) {
@@ -38,7 +38,7 @@ __global__ __launch_bounds__(64 * NWB) void k_step_fwd(const LayerK a) {
   }
   const float* a0 = KS == 0 && a.a0 ? a.a0 + (int64_t)chain * a.ws_cs + (int64_t)(row0 + lr) * R : nullptr;
   __syncthreads();
-  DGPRF_STAMP(stamp_base, 2);
+  STEP_STAMP(stamp_base, 2);
 
   float xf[8];
 #pragma unroll
@@ -48,7 +48,7 @@ __global__ __launch_bounds__(64 * NWB) void k_step_fwd(const LayerK a) {
 #pragma unroll
   for (int ot = 0; ot < NOT; ++ot) acc[ot] = acs[ot] = f4zero();
   float acc1 = 0.f;  // G1: per-lane partial of F[row lr]
-  DGPRF_STAMP(stamp_base, 6);
+  STEP_STAMP(stamp_base, 6);
   for (int i = 0; i < nit; ++i) {
     const int f0 = chunk_f0(i);
     if (f0 >= R) break;
@@ -86,7 +86,7 @@ __global__ __launch_bounds__(64 * NWB) void k_step_fwd(const LayerK a) {
         }
     }
   }
-  DGPRF_STAMP(stamp_base, 7);
+  STEP_STAMP(stamp_base, 7);
   // acc[ot][r] = F[row lr][ot*16 + 4lq + r]; sum the 4 waves' feature chunks in LDS.  Row stride
   // GPS = 16 NOT + 4: the 16-byte row writes of 8 lanes (one LDS cycle group) start 4 banks apart
   // (a stride of 16 NOT put all 16 rows on one bank: 16-way conflicts)
@@ -101,7 +101,7 @@ __global__ __launch_bounds__(64 * NWB) void k_step_fwd(const LayerK a) {
     for (int ot = 0; ot < NOT; ++ot)
       *reinterpret_cast<f4*>(redw + lr * GPS + ot * 16 + 4 * lq) = acc[ot] + acs[ot];
   }
-  DGPRF_STAMP(stamp_base, 3);
+  STEP_STAMP(stamp_base, 3);
   __syncthreads();
   float* fp = a.fout + (int64_t)chain * a.ws_cs + (int64_t)sl * B * g;
   for (int e = threadIdx.x; e < TR * g; e += blockDim.x) {
@@ -116,7 +116,7 @@ __global__ __launch_bounds__(64 * NWB) void k_step_fwd(const LayerK a) {
 #ifdef DGPRF_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
-  DGPRF_STAMP(stamp_base, 14);
+  STEP_STAMP(stamp_base, 14);
 }
 
 // forward: KS x NOT x RBF x G1 x waves per workgroup (8 / 16 for slices of >= 2 chunks per wave:

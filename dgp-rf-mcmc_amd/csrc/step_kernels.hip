@@ -579,6 +579,7 @@ extern "C" int dgprf_debug_read_stamps(unsigned long long* host, long long n) {
 }
 extern "C" int dgprf_debug_clear_stamps(void) {
   static unsigned long long zeros[17 * 4096 * DGPRF_STAMP_SLOTS];
+  if (g_rg_stamps) (void)hipMemset(g_rg_stamps, 0, (size_t)17 * 4096 * 16 * 8);
   return hipMemcpyToSymbol(HIP_SYMBOL(g_dgprf_stamps), zeros, sizeof(zeros), 0,
                            hipMemcpyHostToDevice) == hipSuccess ? 0 : -3;
 }
@@ -625,6 +626,9 @@ hipError_t launch_step_fwd(const dgprf_plan_t& pl, const StepDev& sd, int layer,
   const int nwf = (w8 && pl.cpw[layer] % 8 == 0) ? 16 : (w8 ? 8 : 4);
   int lds_floats = 0;
   LayerK a = make_layer_k(pl, sd, layer, lds_floats, false, nwf);
+#ifdef DGPRF_STAMPS
+  a.stamps = rg_stamp_buffer();
+#endif
   // wide first layer: A_1 = X Omega_1 first — unless the rows were gathered from the dataset's
   // resident projection (sd.bd.A1)
   if (a.a0 && with_agemm && !sd.bd.A1) {
@@ -731,6 +735,9 @@ hipError_t launch_step_bwd(const dgprf_plan_t& pl, const StepDev& sd, int layer,
     lds_floats = 0;
     a = make_layer_k(pl, sd, layer, lds_floats, /*bwd=*/true, 4);
   }
+#ifdef DGPRF_STAMPS
+  a.stamps = rg_stamp_buffer();
+#endif
   dim3 grid(a.main_blocks, 1, pl.n_chains);
   k_step_bwd_launch(pl.d[layer], pl.n_gp[layer], pl.kind[layer] == DGPRF_RBF, sd.full_bayes != 0,
                     w8, grid, (size_t)lds_floats * sizeof(float), s, a);

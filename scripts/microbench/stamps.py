@@ -22,8 +22,16 @@ from models.regression_model import RegressionDGP  # noqa: E402
 
 SLOTS = 16
 dev = torch.device("cuda", 0)
-CFG = 5 if "--config5" in sys.argv else 2  # config 5: L=5 mixed RBF/ARC, n_rf=8192, g=16
-if CFG == 5:
+CFG = 5 if "--config5" in sys.argv else (4 if "--config4" in sys.argv else 2)
+if CFG == 4:  # config 4: 4 x RBF, n_rf 4096, g [30, 30, 30, 10], 784 inputs, softmax
+    from dgprf.data import CONFIGS, classification_data  # noqa: E402
+    from likelihoods import Softmax  # noqa: E402
+    from models.dgp import DGP_RF  # noqa: E402
+    c = CONFIGS[4]
+    X, Y = classification_data(c["n"], c["d_in"], c["d_out"], seed=0, device=dev)
+    m = DGP_RF(c["d_in"], c["d_out"], n_hidden_layers=len(c["kinds"]), n_rf=c["n_rf"],
+               n_gp=c["n_gp"], likelihood=Softmax(), kernel_type_list=c["kinds"])
+elif CFG == 5:  # config 5: L=5 mixed RBF/ARC, n_rf=8192, g=16
     X, Y, _ = regression_data(1_000_000, 16, 0, device=dev)
     m = RegressionDGP(16, 1, n_hidden_layers=5, n_rf=8192, n_gp=[16, 16, 16, 16, 1],
                       likelihood=Gaussian(), kernel_type_list=["RBF", "ARC", "RBF", "ARC", "RBF"])
@@ -31,20 +39,27 @@ else:
     X, Y, _ = regression_data(1_000_000, 8, 0, device=dev)
     m = RegressionDGP(8, 1, n_hidden_layers=3, n_rf=1024, n_gp=[8, 8, 1], likelihood=Gaussian())
 FB = "--full-bayes" in sys.argv  # full_bayesian=True steps; hyper workgroups reported apart
-m.precond_update(None, 1_000_000, precond_type="identity", full_bayesian=FB)
+NDATA = X.shape[0]
+m.precond_update(None, NDATA, precond_type="identity", full_bayesian=FB)
 eng = m._engine
 lib = N.lib()
 for _ in range(50):
-    eng.step(X, Y, 1_000_000, 0.01, 0.9, 1.0, batch_size=200, mode=2, full_bayes=FB)
+    eng.step(X, Y, NDATA, 0.01, 0.9, 1.0, batch_size=200, mode=2, full_bayes=FB)
 torch.cuda.synchronize()
 lib.dgprf_debug_clear_stamps()
 for _ in range(3):
-    eng.step(X, Y, 1_000_000, 0.01, 0.9, 1.0, batch_size=200, mode=2, full_bayes=FB)
+    eng.step(X, Y, NDATA, 0.01, 0.9, 1.0, batch_size=200, mode=2, full_bayes=FB)
 torch.cuda.synchronize()
 n = 17 * 4096 * SLOTS
 buf = (ctypes.c_ulonglong * n)()
 assert lib.dgprf_debug_read_stamps(buf, n) == 0
 S = np.frombuffer(buf, dtype=np.uint64).reshape(17, 4096, SLOTS).astype(np.int64)
+# the per-tile forward / backward kernels stamp into the launcher's buffer (a.stamps)
+buf2 = (ctypes.c_ulonglong * n)()
+lib.dgprf_debug_read_rg_stamps.argtypes = [ctypes.c_void_p, ctypes.c_longlong]
+if lib.dgprf_debug_read_rg_stamps(buf2, n) == 0:
+    S2 = np.frombuffer(buf2, dtype=np.uint64).reshape(17, 4096, SLOTS).astype(np.int64)
+    S = np.where(S2 > 0, S2, S)
 Lm = m.n_hidden_layers
 names = {2 * l: f"fwd{l}" for l in range(Lm)}
 names.update({2 * l + 1: f"bwd{l}" for l in range(Lm)})
