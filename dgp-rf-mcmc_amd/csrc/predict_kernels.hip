@@ -1023,6 +1023,7 @@ void k_forward_tiles(
   }
   for (int e = lane; e < TPW * TR * T.ftst; e += 64) ftw[e] = 0.f;
   __syncthreads();
+  if (L < 4) DGPRF_PST(4, __builtin_amdgcn_s_memtime());  // input rows staged
   for (int layer = 0; layer < L; ++layer) {
     const float* __restrict__ om = omega + ochain + pl.omega_off[layer];
     const float* __restrict__ W = Wc + pl.w_off[layer];
@@ -1136,6 +1137,8 @@ void k_forward_pairs(const dgprf_plan_t pl, const float* __restrict__ thetas, co
   float* ftw0 = smem + T.f_off + (2 * wave) * round4(TR * T.ftst);
   float* ftw1 = smem + T.f_off + (2 * wave + 1) * round4(TR * T.ftst);
   const int L = pl.n_layers;
+  DGPRF_PST(0, __builtin_amdgcn_s_memrealtime());
+  DGPRF_PST(7, __builtin_amdgcn_s_memtime());
   for (int e = lane; e < TR * T.xin_st; e += 64) {
     const int r = e / T.xin_st, k = e - r * T.xin_st;
     const int64_t b = wrow0 + r;
@@ -1151,6 +1154,7 @@ void k_forward_pairs(const dgprf_plan_t pl, const float* __restrict__ thetas, co
       tile_layer0_pair<true>(pl, W0, W1, om0, der[dchain], T, smem, xin, ftw0, ftw1, lr, lq);
     else
       tile_layer0_pair<false>(pl, W0, W1, om0, der[dchain], T, smem, xin, ftw0, ftw1, lr, lq);
+    DGPRF_PST(1, __builtin_amdgcn_s_memtime());
     // unrolled: each sample's copy of layers >= 1 keeps only its own state live (a loop over the
     // two samples spilled 5 VGPRs at the 96-register budget; unrolled: 92, none spilled)
 #pragma unroll
@@ -1202,8 +1206,10 @@ void k_forward_pairs(const dgprf_plan_t pl, const float* __restrict__ thetas, co
         lse_m[idx] = m1;
         if (se_sum) se_sum[idx] += se;
       }
+      DGPRF_PST(2 + j, __builtin_amdgcn_s_memtime());
     }
   }
+  DGPRF_PST(6, __builtin_amdgcn_s_memrealtime());
 }
 
 }  // namespace

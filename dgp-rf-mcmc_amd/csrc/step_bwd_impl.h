@@ -510,13 +510,15 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
       if (dt < ND) *reinterpret_cast<f4*>(redw + lr * DPS + dt * 16 + 4 * lq) = dxa[dt];
     __syncthreads();
     float* dxp = a.dxout + (int64_t)chain * a.ws_cs + (int64_t)sl * B * dxw;
+    // write-through (sc1), as the forward's F partials
+    const rsrc_t rdx = make_rsrc(dxp, (int64_t)B * dxw);
     for (int e = threadIdx.x; e < TR * dxw; e += blockDim.x) {
       const int r = e / dxw, k = e - r * dxw, b = row0 + r;
       if (b < B) {
         float v = red[r * DPS + k];
 #pragma unroll
         for (int w = 1; w < NWB; ++w) v += red[w * TR * DPS + r * DPS + k];
-        dxp[(int64_t)b * dxw + k] = v;
+        bstore1_wt(v, rdx, (uint32_t)(((int64_t)b * dxw + k) * 4));
       }
     }
   }

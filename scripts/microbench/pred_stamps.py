@@ -23,16 +23,35 @@ from dgprf.predictive import PredictiveLSE  # noqa: E402
 from likelihoods import Gaussian  # noqa: E402
 from models.regression_model import RegressionDGP  # noqa: E402
 
-n_test = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000
+n_test = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 100_000
 dev = torch.device("cuda", 0)
 _, _, a = regression_data(1000, 8, seed=0, device=dev)
 Xt, Yt, _ = regression_data(n_test, 8, seed=1, device=dev, a=a)
 E.set_seed(2)
 m = RegressionDGP(8, 1, n_hidden_layers=3, n_rf=1024, n_gp=[8, 8, 1], likelihood=Gaussian())
 m.precond_update(None, 1_000_000, precond_type="identity")
+def _arg(name, dflt=0):
+    return int(sys.argv[sys.argv.index(name) + 1]) if name in sys.argv else dflt
+
+
+# placement probes: move Omega / theta by a number of floats inside a larger allocation
+eng = m._engine
+for nm, k in (("omega", _arg("--om-shift")), ("theta", _arg("--th-shift"))):
+    if k:
+        t = getattr(eng, nm)
+        big = torch.empty(t.numel() + k, dtype=t.dtype, device=t.device)
+        v = big[k:k + t.numel()].view(t.shape)
+        v.copy_(t)
+        setattr(eng, nm, v)
+        print(f"{nm} moved by {k} floats", flush=True)
 acc = PredictiveLSE(m._engine, Xt, Yt)
+PAIRS = "--pairs" in sys.argv  # k_forward_pairs: slots 1 / 2 / 3 = after layer 0, sample 0, sample 1
 for _ in range(3):
-    acc.add_sample()
+    if PAIRS:
+        th = m._engine.theta
+        acc.add_samples(torch.stack([th, th]))
+    else:
+        acc.add_sample()
 torch.cuda.synchronize()
 nw = (n_test + 15) // 16
 nw = (nw + 15) // 16 * 16
@@ -50,8 +69,12 @@ lay = np.stack([st[:, 1] - st[:, 7], st[:, 2] - st[:, 1], st[:, 3] - st[:, 2]], 
 print(f"waves {len(st)}  kernel span {span_us:.1f} us (realtime)")
 print(f"wave lifetime cycles: median {np.median(life):.0f}  p10 {np.percentile(life, 10):.0f}  "
       f"p90 {np.percentile(life, 90):.0f}  max {life.max()}")
-print("per-layer cycles (median):", [int(np.median(lay[:, i])) for i in range(3)])
+print("per-layer cycles (median):" if not PAIRS else
+      "cycles (median) [layer 0 of the pair, sample 0 layers >= 1, sample 1 layers >= 1]:",
+      [int(np.median(lay[:, i])) for i in range(3)])
 print(f"wave realtime life us: median {np.median(rt1 - rt0) / 100:.1f}")
+if not PAIRS:
+    print("input staging cycles (entry -> rows in LDS), median:", int(np.median(st[:, 4] - st[:, 7])))
 hw = st[:, 5] & 0xFFFFFFFF
 xcc = st[:, 5] >> 32
 simd = (hw >> 4) & 3
