@@ -968,6 +968,13 @@ __device__ __forceinline__ void tile_layer0_pair(const dgprf_plan_t& pl, const f
 // the product): slot 0 = s_memrealtime at entry, 7 = s_memtime at entry, 1..4 = s_memtime after
 // each layer, 6 = s_memrealtime at exit, 5 = HW_ID | XCC_ID << 32.
 #ifdef DGPRF_PSTAMPS
+// DGPRF_PST_REAL: the per-layer stamps (slots 1..4, 7) in s_memrealtime ticks (100 MHz) instead of
+// shader cycles, to tell clock changes from work changes
+#ifdef DGPRF_PST_REAL
+#define PST_CLK() __builtin_amdgcn_s_memrealtime()
+#else
+#define PST_CLK() __builtin_amdgcn_s_memtime()
+#endif
 __device__ unsigned long long g_pred_stamps[1 << 20];
 #define DGPRF_PST(i, v)                                                        \
   do {                                                                         \
@@ -1012,7 +1019,7 @@ void k_forward_tiles(
   const float* Wc = theta + (int64_t)chain * pl.w_total;
   const int L = pl.n_layers;
   DGPRF_PST(0, __builtin_amdgcn_s_memrealtime());
-  DGPRF_PST(7, __builtin_amdgcn_s_memtime());
+  DGPRF_PST(7, PST_CLK());
   DGPRF_PST(5, (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4) |
                    ((unsigned long long)__builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20) << 32));
   // this wave's X rows (zero past n)
@@ -1023,7 +1030,7 @@ void k_forward_tiles(
   }
   for (int e = lane; e < TPW * TR * T.ftst; e += 64) ftw[e] = 0.f;
   __syncthreads();
-  if (L < 4) DGPRF_PST(4, __builtin_amdgcn_s_memtime());  // input rows staged
+  if (L < 4) DGPRF_PST(4, PST_CLK());  // input rows staged
   for (int layer = 0; layer < L; ++layer) {
     const float* __restrict__ om = omega + ochain + pl.omega_off[layer];
     const float* __restrict__ W = Wc + pl.w_off[layer];
@@ -1066,7 +1073,7 @@ void k_forward_tiles(
       else DGPRF_TL((NOTMAX >= 4 ? 4 : 1), false, false, false);
     }
 #undef DGPRF_TL
-    if (layer < 4) DGPRF_PST(1 + layer, __builtin_amdgcn_s_memtime());
+    if (layer < 4) DGPRF_PST(1 + layer, PST_CLK());
   }
   // likelihood per row: lanes 0..15 of each wave, row lr of each of the wave's tiles
   const bool want_lik = logp_out || se_out || lse_m;
@@ -1138,7 +1145,7 @@ void k_forward_pairs(const dgprf_plan_t pl, const float* __restrict__ thetas, co
   float* ftw1 = smem + T.f_off + (2 * wave + 1) * round4(TR * T.ftst);
   const int L = pl.n_layers;
   DGPRF_PST(0, __builtin_amdgcn_s_memrealtime());
-  DGPRF_PST(7, __builtin_amdgcn_s_memtime());
+  DGPRF_PST(7, PST_CLK());
   for (int e = lane; e < TR * T.xin_st; e += 64) {
     const int r = e / T.xin_st, k = e - r * T.xin_st;
     const int64_t b = wrow0 + r;
@@ -1154,7 +1161,7 @@ void k_forward_pairs(const dgprf_plan_t pl, const float* __restrict__ thetas, co
       tile_layer0_pair<true>(pl, W0, W1, om0, der[dchain], T, smem, xin, ftw0, ftw1, lr, lq);
     else
       tile_layer0_pair<false>(pl, W0, W1, om0, der[dchain], T, smem, xin, ftw0, ftw1, lr, lq);
-    DGPRF_PST(1, __builtin_amdgcn_s_memtime());
+    DGPRF_PST(1, PST_CLK());
     // unrolled: each sample's copy of layers >= 1 keeps only its own state live (a loop over the
     // two samples spilled 5 VGPRs at the 96-register budget; unrolled: 92, none spilled)
 #pragma unroll
@@ -1206,7 +1213,7 @@ void k_forward_pairs(const dgprf_plan_t pl, const float* __restrict__ thetas, co
         lse_m[idx] = m1;
         if (se_sum) se_sum[idx] += se;
       }
-      DGPRF_PST(2 + j, __builtin_amdgcn_s_memtime());
+      DGPRF_PST(2 + j, PST_CLK());
     }
   }
   DGPRF_PST(6, __builtin_amdgcn_s_memrealtime());

@@ -28,7 +28,10 @@ dev = torch.device("cuda", 0)
 _, _, a = regression_data(1000, 8, seed=0, device=dev)
 Xt, Yt, _ = regression_data(n_test, 8, seed=1, device=dev, a=a)
 E.set_seed(2)
-m = RegressionDGP(8, 1, n_hidden_layers=3, n_rf=1024, n_gp=[8, 8, 1], likelihood=Gaussian())
+NL = int(sys.argv[sys.argv.index("--layers") + 1]) if "--layers" in sys.argv else 3
+m = RegressionDGP(8, 1, n_hidden_layers=NL, n_rf=1024, n_gp=[8] * (NL - 1) + [1], likelihood=Gaussian())
+if "--xscale" in sys.argv:  # probe: scale the test inputs (data-dependence of layer 0's time)
+    Xt = Xt * float(sys.argv[sys.argv.index("--xscale") + 1])
 m.precond_update(None, 1_000_000, precond_type="identity")
 def _arg(name, dflt=0):
     return int(sys.argv[sys.argv.index(name) + 1]) if name in sys.argv else dflt
