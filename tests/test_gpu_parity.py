@@ -664,6 +664,12 @@ def test_precond_rmsprop_masses(dev, golden):
     (["RBF", "RBF"], [100, 17], [30, 2], 100, False, "gaussian", 33),  # large-d path, 2 out tiles
     (["ARC", "RBF"], [64, 64], [16, 5], 40, True, "softmax", 200),      # input_cat, wide d
     (["RBF"] * 3, [1024] * 3, [8, 8, 1], 8, False, "gaussian", 200),   # config 2 shapes
+    # n_rf 4096: 8-wave whole-slice backward, gW tiles of g % 16 != 0 staged through LDS (g = 10,
+    # 2, 48), a d > 32 hidden layer (KS = 0), and g = 60, whose staging does not fit next to the
+    # slice image (the 4-wave form instead)
+    (["ARC", "RBF"], [4096, 4096], [10, 2], 6, False, "gaussian", 64),
+    (["RBF", "RBF"], [4096, 4096], [48, 3], 12, False, "gaussian", 40),
+    (["RBF"], [4096], [60], 5, False, "softmax", 20),
 ])
 def test_edge_shapes_forward_and_grad(dev, kinds, n_rf, n_gp, d_in, cat, lik, B):
     from likelihoods import Gaussian, Softmax
