@@ -524,6 +524,7 @@ __host__ __device__ constexpr int tw_wst(int notm) { return 16 * notm + 4; }  //
 
 struct TileLds {
   int obuf, wbuf, o_off, w_off, xin_off, xin_st, f_off, ftst, total;
+  int orows;  // Omega rows staged per block (16 njo; 8 in the pair kernel, whose layers have d <= 8)
 };
 
 // the pair kernel's layer-0 W rows: [half][feature][s * 8 + o], row stride PST = 16.  (A stride of
@@ -536,7 +537,10 @@ __host__ __device__ inline TileLds tile_lds(const dgprf_plan_t& pl, int notmax, 
   int gmax = 1;
   for (int l = 0; l < pl.n_layers; ++l) gmax = pl.n_gp[l] > gmax ? pl.n_gp[l] : gmax;
   TileLds T;
-  T.obuf = 16 * njo * TW_OST;               // njo float4 per thread: 16 Omega rows each
+  // njo float4 per thread: 16 Omega rows each; the pair kernel (every layer d <= 8, two k-steps)
+  // stages the 8 rows its k-steps read, so five of its workgroups fit a CU's 160 KiB with room
+  T.orows = spw == 2 ? 8 : 16 * njo;
+  T.obuf = T.orows * TW_OST;
   // [cos|sin][64 features][16 NOT + 4]; notmax = 0 (the lean instance: every layer g <= 8, d <= 8)
   // [cos|sin][64 features][8] (G8) or [cos|sin][64] (g == 1)
   T.wbuf = notmax == 0 ? (spw == 2 ? 2 * 64 * PST : 2 * 64 * 8) : 2 * 64 * tw_wst(notmax);
@@ -656,8 +660,9 @@ __device__ __forceinline__ void tile_layer(const dgprf_plan_t& pl, int layer,
 #pragma unroll
     for (int j = 0; j < JO; ++j) {
       const int i = tid + 256 * j;
-      *reinterpret_cast<f4*>(osb + (i >> 4) * TW_OST + 4 * (i & 15)) =
-          REV ? so[j] * 0.15915494309189535f : so[j];
+      if ((i >> 4) < T.orows)
+        *reinterpret_cast<f4*>(osb + (i >> 4) * TW_OST + 4 * (i & 15)) =
+            REV ? so[j] * 0.15915494309189535f : so[j];
     }
   };
 
@@ -907,8 +912,9 @@ __device__ __forceinline__ void tile_layer0_pair(const dgprf_plan_t& pl, const f
         }
       }
     }
-    *reinterpret_cast<f4*>(osb + (tid >> 4) * TW_OST + 4 * (tid & 15)) =
-        REV ? so * 0.15915494309189535f : so;
+    if ((tid >> 4) < T.orows)
+      *reinterpret_cast<f4*>(osb + (tid >> 4) * TW_OST + 4 * (tid & 15)) =
+          REV ? so * 0.15915494309189535f : so;
   };
   f4 acc = f4zero(), acs = f4zero();
   const int nb = (R + 63) >> 6;
