@@ -514,7 +514,18 @@ int dgprf_forward_samples(const dgprf_plan_t* plan, const float* thetas, int32_t
   if (scratch_floats < 0 || (scratch_floats > 0 && !scratch)) return DGPRF_E_ARG;
   if (!A1 && scratch_floats < dgprf::forward_cfg(*plan, n).scratch_floats) return DGPRF_E_ARG;
   return hip_rc(dgprf::launch_forward_samples(*plan, thetas, n_samples, omega, der, X, A1, Y, y_cols,
-                                              n, lse_m, lse_s, se_sum, scratch, as_stream(stream)));
+                                              n, lse_m, lse_s, se_sum, scratch, scratch_floats,
+                                              as_stream(stream)));
+}
+
+int dgprf_forward_samples_scratch(const dgprf_plan_t* plan, int64_t n, int32_t n_samples,
+                                  int64_t* floats_out) {
+  int rc = check_plan(plan);
+  if (rc) return rc;
+  if (!floats_out || n < 0 || n_samples < 1) return DGPRF_E_ARG;
+  *floats_out = std::max(dgprf::forward_cfg(*plan, n).scratch_floats,
+                         dgprf::forward_samples_scratch(*plan, n, n_samples));
+  return DGPRF_OK;
 }
 
 int dgprf_lse_finalize(const float* lse_m, const float* lse_s, const float* se_sum, int32_t parts,

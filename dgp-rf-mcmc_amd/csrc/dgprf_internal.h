@@ -139,16 +139,20 @@ hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const
                                const float* der, const float* X, const float* Y, int y_cols,
                                int64_t n, float* const* f_out, float* logp, float* se,
                                float* lse_m, float* lse_s, float* se_sum, float* scratch,
-                               hipStream_t s, const float* a1_full = nullptr);
+                               hipStream_t s, const float* a1_full = nullptr, int n_samples = 1);
 // (a1_full: X Omega_1 of all n rows, precomputed by the caller for a wide first layer: no A_1 GEMM)
 // Posterior-predictive LSE fold of n_samples samples of every chain (thetas [n_samples][C][w_total]),
-// sample order: two samples per pass of the pair kernel for lean models (layer 0 shared), else one
+// sample order: two samples per pass of the pair kernel for lean models (layer 0 shared) — every
+// pair in one launch when scratch holds forward_samples_scratch floats — else one
 // launch_forward_rows per sample.
 hipError_t launch_forward_samples(const dgprf_plan_t& pl, const float* thetas, int n_samples,
                                   const float* omega, const float* der, const float* X,
                                   const float* A1, const float* Y, int y_cols, int64_t n, float* lse_m,
-                                  float* lse_s, float* se_sum, float* scratch, hipStream_t s);
+                                  float* lse_s, float* se_sum, float* scratch,
+                                  int64_t scratch_floats, hipStream_t s);
 bool forward_pairs_ok(const dgprf_plan_t& pl, int64_t n);
+// scratch floats that let launch_forward_samples run every pair in one launch (0: not applicable)
+int64_t forward_samples_scratch(const dgprf_plan_t& pl, int64_t n, int n_samples);
 hipError_t launch_lse_finalize(const float* lse_m, const float* lse_s, const float* se_sum,
                                int parts, int64_t n, double s_total, float log_y_std, float y_std,
                                float* lse_out, double* out, hipStream_t s);

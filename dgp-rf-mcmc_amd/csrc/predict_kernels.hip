@@ -187,6 +187,19 @@ __device__ __forceinline__ void layer_partial(const float* __restrict__ om,
   }
 }
 
+// One sample's log p (and squared error) of row idx folded into the online log-sum-exp
+// accumulators (experiments/utils_training.py:79-85): m' = max(m, lp), s' = s e^{m-m'} + e^{lp-m'}.
+// The pair kernel's in-place fold and k_lse_fold_samples share it, so both give the same bits.
+__device__ __forceinline__ void lse_fold1(float* __restrict__ lse_m, float* __restrict__ lse_s,
+                                          float* __restrict__ se_sum, int64_t idx, float lp,
+                                          float se) {
+  const float m0 = lse_m[idx], s0 = lse_s[idx];
+  const float m1 = fmaxf(m0, lp);
+  lse_s[idx] = s0 * expf(m0 - m1) + expf(lp - m1);
+  lse_m[idx] = m1;
+  if (se_sum) se_sum[idx] += se;
+}
+
 // One workgroup = one 16-row tile; its NWR waves split each layer's RF features (16-feature chunks
 // w, w + NWR, ...) and the per-wave F partials are summed in LDS in wave order.  NWR = 16 (4 waves
 // per SIMD) for test sets too small to fill the chip with the one-wave-per-tile tile kernel.
@@ -221,7 +234,7 @@ void k_forward_rows(
   float* xs = smem;
   float* red = smem + LD.red_off;
   float* ft = smem + LD.ft_off;
-  const float* Wc = theta + (int64_t)chain * pl.w_total;
+  const float* Wc = theta + ((int64_t)blockIdx.z * pl.n_chains + chain) * pl.w_total;
   const int L = pl.n_layers;
 
   for (int layer = 0; layer < L; ++layer) {
@@ -329,15 +342,11 @@ void k_forward_rows(
         lp = lab_ok ? f[lab] - (mx + logf(s)) : __builtin_nanf("");
       }
       const int64_t idx = (int64_t)chain * n + b;
-      if (logp_out) logp_out[idx] = lp;
-      if (se_out) se_out[idx] = se;
-      if (lse_m) {
-        const float m0 = lse_m[idx], s0 = lse_s[idx];
-        const float m1 = fmaxf(m0, lp);
-        lse_s[idx] = s0 * expf(m0 - m1) + expf(lp - m1);
-        lse_m[idx] = m1;
-        if (se_sum) se_sum[idx] += se;
-      }
+      // blockIdx.z = sample of a multi-sample launch: its outputs [sample][chain][n]
+      const int64_t oidx = (int64_t)blockIdx.z * pl.n_chains * n + idx;
+      if (logp_out) logp_out[oidx] = lp;
+      if (se_out) se_out[oidx] = se;
+      if (lse_m) lse_fold1(lse_m, lse_s, se_sum, idx, lp, se);
     }
   }
 }
@@ -1022,7 +1031,7 @@ void k_forward_tiles(
   const int64_t wrow0 = row_begin + (int64_t)blockIdx.x * TW_ROWS * TPW + wave * TR * TPW;
   float* xin = smem + T.xin_off + wave * TPW * TR * T.xin_st;
   float* ftw = smem + T.f_off + wave * round4(TPW * TR * T.ftst);
-  const float* Wc = theta + (int64_t)chain * pl.w_total;
+  const float* Wc = theta + ((int64_t)blockIdx.z * pl.n_chains + chain) * pl.w_total;
   const int L = pl.n_layers;
   DGPRF_PST(0, __builtin_amdgcn_s_memrealtime());
   DGPRF_PST(7, PST_CLK());
@@ -1110,15 +1119,11 @@ void k_forward_tiles(
         lp = lab_ok ? f[lab] - (mx + logf(s)) : __builtin_nanf("");
       }
       const int64_t idx = (int64_t)chain * n + b;
-      if (logp_out) logp_out[idx] = lp;
-      if (se_out) se_out[idx] = se;
-      if (lse_m) {
-        const float m0 = lse_m[idx], s0 = lse_s[idx];
-        const float m1 = fmaxf(m0, lp);
-        lse_s[idx] = s0 * expf(m0 - m1) + expf(lp - m1);
-        lse_m[idx] = m1;
-        if (se_sum) se_sum[idx] += se;
-      }
+      // blockIdx.z = sample of a multi-sample launch: its outputs [sample][chain][n]
+      const int64_t oidx = (int64_t)blockIdx.z * pl.n_chains * n + idx;
+      if (logp_out) logp_out[oidx] = lp;
+      if (se_out) se_out[oidx] = se;
+      if (lse_m) lse_fold1(lse_m, lse_s, se_sum, idx, lp, se);
     }
   }
   DGPRF_PST(6, __builtin_amdgcn_s_memrealtime());
@@ -1131,14 +1136,17 @@ void k_forward_tiles(
 // A workgroup covers 64 test rows of one chain, so each accumulator element has one writer.
 // Same register budget as the lean one-sample instance.
 __global__ __launch_bounds__(TW_THREADS) __attribute__((amdgpu_waves_per_eu(TILE_LEAN_WAVES)))
-void k_forward_pairs(const dgprf_plan_t pl, const float* __restrict__ thetas, const int two,
+void k_forward_pairs(const dgprf_plan_t pl, const float* __restrict__ thetas, const int n_samples,
                      const float* __restrict__ omega, const float* __restrict__ der,
                      const float* __restrict__ X, const float* __restrict__ Y, const int y_cols,
                      const int64_t n, float* __restrict__ lse_m, float* __restrict__ lse_s,
-                     float* __restrict__ se_sum) {
+                     float* __restrict__ se_sum, float* __restrict__ lp_out,
+                     float* __restrict__ se_out) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const TileLds T = tile_lds(pl, 0, 1, 1, false, 2);
   const int chain = blockIdx.y, C = pl.n_chains;
+  // pair blockIdx.z: samples s0 = 2 z and s0 + 1 (when s0 + 1 < n_samples) of thetas
+  const int s0 = 2 * (int)blockIdx.z, two = s0 + 1 < n_samples ? 1 : 0;
   const int64_t ochain = pl.hyp_per_chain ? (int64_t)chain * pl.omega_total : 0;
   const int64_t dchain = pl.hyp_per_chain ? (int64_t)chain * pl.der_total : 0;
   // the wave index through readfirstlane: the wave's LDS tiles / row base are SGPR values, not
@@ -1161,7 +1169,7 @@ void k_forward_pairs(const dgprf_plan_t pl, const float* __restrict__ thetas, co
   __syncthreads();
   const float* om0 = omega + ochain + pl.omega_off[0];
   {
-    const float* W0 = thetas + (int64_t)chain * pl.w_total;
+    const float* W0 = thetas + ((int64_t)s0 * C + chain) * pl.w_total;
     const float* W1 = two ? W0 + (int64_t)C * pl.w_total : W0;
     if (pl.kind[0] == DGPRF_RBF)
       tile_layer0_pair<true>(pl, W0, W1, om0, der[dchain], T, smem, xin, ftw0, ftw1, lr, lq);
@@ -1213,16 +1221,33 @@ void k_forward_pairs(const dgprf_plan_t pl, const float* __restrict__ thetas, co
           lp = (lab >= 0 && lab < g) ? f[lab] - (mx + logf(sm)) : __builtin_nanf("");
         }
         const int64_t idx = (int64_t)chain * n + b;
-        const float m0 = lse_m[idx], s0 = lse_s[idx];
-        const float m1 = fmaxf(m0, lp);
-        lse_s[idx] = s0 * expf(m0 - m1) + expf(lp - m1);
-        lse_m[idx] = m1;
-        if (se_sum) se_sum[idx] += se;
+        if (lp_out) {  // every pair of the call in one launch: [sample][chain][n], folded after
+          const int64_t o = (int64_t)(s0 + j) * C * n + idx;
+          lp_out[o] = lp;
+          if (se_out) se_out[o] = se;
+        } else {
+          lse_fold1(lse_m, lse_s, se_sum, idx, lp, se);
+        }
       }
       DGPRF_PST(2 + j, PST_CLK());
     }
   }
   DGPRF_PST(6, __builtin_amdgcn_s_memrealtime());
+}
+
+// The per-row log p / squared errors of n_samples samples ([sample][chain][n], one multi-pair
+// launch) folded into the accumulators in sample order — the same sequence of lse_fold1 steps the
+// one-pair-per-launch path takes, so the same bits.
+__global__ __launch_bounds__(256) void k_lse_fold_samples(const float* __restrict__ lp,
+                                                          const float* __restrict__ se,
+                                                          int n_samples, int64_t cn,
+                                                          float* __restrict__ lse_m,
+                                                          float* __restrict__ lse_s,
+                                                          float* __restrict__ se_sum) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= cn) return;
+  for (int j = 0; j < n_samples; ++j)
+    lse_fold1(lse_m, lse_s, se_sum, idx, lp[j * cn + idx], se ? se[j * cn + idx] : 0.f);
 }
 
 }  // namespace
@@ -1311,8 +1336,11 @@ hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const
                                const float* der, const float* X, const float* Y, int y_cols,
                                int64_t n, float* const* f_out, float* logp, float* se,
                                float* lse_m, float* lse_s, float* se_sum, float* scratch,
-                               hipStream_t s, const float* a1_full) {
+                               hipStream_t s, const float* a1_full, int n_samples) {
   if (n <= 0) return hipSuccess;
+  // n_samples > 1: theta holds that many samples ([n_samples][C][w_total]), one per grid.z, and
+  // logp / se receive [n_samples][C][n] (no in-kernel fold: the caller folds in sample order)
+  if (n_samples > 1 && (lse_m || (f_out && f_out[0]))) return hipErrorInvalidValue;
   FOut fo;
   for (int l = 0; l < DGPRF_MAX_LAYERS; ++l) fo.p[l] = (f_out && l < pl.n_layers) ? f_out[l] : nullptr;
   bool smalld = true;
@@ -1353,7 +1381,7 @@ hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const
       for (int l = 0; l < pl.n_layers; ++l) lean = lean && pl.n_gp[l] <= 8 && pl.d[l] <= 8;
       if (lean) ntm = 0;
       const TileLds T = tile_lds(pl, ntm, njo, tpw, wide0);
-      dim3 tgrid((unsigned)((nr + TW_ROWS * tpw - 1) / (TW_ROWS * tpw)), pl.n_chains);
+      dim3 tgrid((unsigned)((nr + TW_ROWS * tpw - 1) / (TW_ROWS * tpw)), pl.n_chains, n_samples);
       const size_t tl = (size_t)T.total * sizeof(float);
 #define DGPRF_TILE_LAUNCH1(NM, J, JO, TP, WD)                                                      \
   do {                                                                                             \
@@ -1385,7 +1413,7 @@ hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const
     } else {
       const int nwr = cfg.rows_waves, tt = cfg.rows_tt;
       const size_t lds = (size_t)fwd_lds(pl, nwr, tt).total * sizeof(float);
-      dim3 grid((unsigned)((nr + TR * tt - 1) / (TR * tt)), pl.n_chains);
+      dim3 grid((unsigned)((nr + TR * tt - 1) / (TR * tt)), pl.n_chains, n_samples);
 #define DGPRF_FWD_LAUNCH_W(S, NM, NWR_)                                                             \
   do {                                                                                             \
     set_lds_limit((const void*)k_forward_rows<S, NM, NWR_>, lds);                                  \
@@ -1434,13 +1462,29 @@ bool forward_pairs_ok(const dgprf_plan_t& pl, int64_t n) {
 hipError_t launch_forward_samples(const dgprf_plan_t& pl, const float* thetas, int n_samples,
                                   const float* omega, const float* der, const float* X,
                                   const float* A1, const float* Y, int y_cols, int64_t n, float* lse_m,
-                                  float* lse_s, float* se_sum, float* scratch, hipStream_t s) {
+                                  float* lse_s, float* se_sum, float* scratch,
+                                  int64_t scratch_floats, hipStream_t s) {
   if (n <= 0 || n_samples <= 0) return hipSuccess;
   // 32-bit buffer offsets across two samples' W
   const bool off_ok = ((int64_t)pl.n_chains * pl.w_total + 2 * (int64_t)pl.n_rf[0] * pl.n_gp[0]) * 4 <
                       ((int64_t)1 << 31);
-  if (!off_ok || !forward_pairs_ok(pl, n)) {  // one launch per sample (sample order)
-    for (int j = 0; j < n_samples; ++j) {
+  if (!off_ok || !forward_pairs_ok(pl, n)) {
+    const int64_t cn = (int64_t)pl.n_chains * n;
+    const int64_t need = forward_samples_scratch(pl, n, n_samples);
+    if (need > 0 && scratch && scratch_floats >= need && (A1 || !forward_cfg(pl, n).wide0)) {
+      // every sample in one launch (grid.z = sample): a small test set's launch leaves most of the
+      // chip idle (config 3: 143 workgroups; config 4: 2.4 rounds of 625), several fill it; the
+      // per-row log p / se go to scratch and the fold applies them in sample order
+      float* lp = scratch;
+      float* se = se_sum ? scratch + (int64_t)n_samples * cn : nullptr;
+      hipError_t e = launch_forward_rows(pl, thetas, omega, der, X, Y, y_cols, n, nullptr, lp, se,
+                                         nullptr, nullptr, nullptr, nullptr, s, A1, n_samples);
+      if (e != hipSuccess) return e;
+      hipLaunchKernelGGL(k_lse_fold_samples, dim3((unsigned)((cn + 255) / 256)), dim3(256), 0, s,
+                         lp, se, n_samples, cn, lse_m, lse_s, se_sum);
+      return hipGetLastError();
+    }
+    for (int j = 0; j < n_samples; ++j) {  // one launch per sample (sample order)
       const hipError_t e = launch_forward_rows(pl, thetas + (int64_t)j * pl.n_chains * pl.w_total,
                                                omega, der, X, Y, y_cols, n, nullptr, nullptr,
                                                nullptr, lse_m, lse_s, se_sum, scratch, s, A1);
@@ -1450,16 +1494,45 @@ hipError_t launch_forward_samples(const dgprf_plan_t& pl, const float* thetas, i
   }
   const TileLds T = tile_lds(pl, 0, 1, 1, false, 2);
   const size_t tl = (size_t)T.total * sizeof(float);
-  dim3 grid((unsigned)((n + TW_ROWS - 1) / TW_ROWS), pl.n_chains);
+  const unsigned tiles = (unsigned)((n + TW_ROWS - 1) / TW_ROWS);
   set_lds_limit((const void*)k_forward_pairs, tl);
-  for (int p = 0; p < n_samples; p += 2) {  // one launch per pair of samples
-    hipLaunchKernelGGL(k_forward_pairs, grid, dim3(TW_THREADS), tl, s, pl,
-                       thetas + (int64_t)p * pl.n_chains * pl.w_total, p + 1 < n_samples ? 1 : 0,
-                       omega, der, X, Y, y_cols, n, lse_m, lse_s, se_sum);
+  const int64_t cn = (int64_t)pl.n_chains * n;
+  const int pairs = (n_samples + 1) / 2;
+  if (pairs > 1 && scratch && scratch_floats >= forward_samples_scratch(pl, n, n_samples)) {
+    // every pair in ONE launch (grid.z = pair): a launch of one pair leaves the chip part-empty for
+    // its last ~40 % (1.22 rounds of resident waves at 1e5 rows); its rows' log p go to scratch
+    // and one fold kernel applies them in sample order
+    float* lp = scratch;
+    float* se = se_sum ? scratch + (int64_t)n_samples * cn : nullptr;
+    hipLaunchKernelGGL(k_forward_pairs, dim3(tiles, pl.n_chains, pairs), dim3(TW_THREADS), tl, s,
+                       pl, thetas, n_samples, omega, der, X, Y, y_cols, n, lse_m, lse_s, se_sum, lp,
+                       se);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_lse_fold_samples, dim3((unsigned)((cn + 255) / 256)), dim3(256), 0, s, lp,
+                       se, n_samples, cn, lse_m, lse_s, se_sum);
+    return hipGetLastError();
+  }
+  for (int p = 0; p < pairs; ++p) {  // one launch per pair of samples, folded in place
+    hipLaunchKernelGGL(k_forward_pairs, dim3(tiles, pl.n_chains, 1), dim3(TW_THREADS), tl, s, pl,
+                       thetas + (int64_t)2 * p * pl.n_chains * pl.w_total,
+                       2 * p + 1 < n_samples ? 2 : 1, omega, der, X, Y, y_cols, n, lse_m, lse_s,
+                       se_sum, nullptr, nullptr);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
+}
+
+// scratch floats the one-launch form of launch_forward_samples needs: log p (and, Gaussian, the
+// squared error) of every sample's rows; 0 when that form does not apply
+int64_t forward_samples_scratch(const dgprf_plan_t& pl, int64_t n, int n_samples) {
+  if (n <= 0) return 0;
+  const int64_t per = (int64_t)pl.n_chains * n * (pl.likelihood == DGPRF_LIK_GAUSSIAN ? 2 : 1);
+  if (forward_pairs_ok(pl, n)) return n_samples >= 3 ? n_samples * per : 0;
+  // one-sample kernels: all samples in one launch (launch_forward_samples takes that form unless
+  // a wide first layer's A_1 would come in scratch chunks, i.e. without a resident projection)
+  return n_samples >= 2 ? n_samples * per : 0;
 }
 
 size_t forward_rows_lds_bytes(const dgprf_plan_t& pl) {

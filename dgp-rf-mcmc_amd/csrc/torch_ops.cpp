@@ -205,7 +205,9 @@ void forward_samples(const Tensor& plan, const Tensor& thetas, const Tensor& ome
   float* a1 = f32o(A1, "A1", (n + 63) / 64 * 64 * (int64_t)pl.n_rf[0]);
   int64_t need = 0;
   check_rc(dgprf_forward_scratch(&pl, n, &need), "dgprf_forward_scratch");
-  float* scr = a1 ? nullptr : f32o(scratch, "scratch", need);
+  // the A_1 chunks need `need` floats unless A1 is resident; more (dgprf_forward_samples_scratch)
+  // lets every sample pair run in one launch
+  float* scr = f32o(scratch, "scratch", a1 ? 0 : need);
   TORCH_CHECK(a1 || need == 0 || scr, "dgprf: forward needs ", need, " floats of scratch");
   check_rc(dgprf_forward_samples(&pl, f32(thetas, "thetas", S * C * pl.w_total), (int32_t)S,
                                  f32(omega, "omega", ch * pl.omega_total),

@@ -22,7 +22,7 @@ RNG_NOISE, RNG_RESAMPLE, RNG_Z, RNG_W, RNG_MOMENTS = 1, 2, 3, 4, 5
 RNG_HYPER, RNG_HYPER_RESAMPLE = 6, 7
 HYP_KERNEL, HYP_LIK, HYP_MEAN = 1, 2, 4
 HMASS = 32  # hmass slots: log_amp l -> l, log_inv_ls l -> 8 + l, mean l -> 16 + l, lik_log_var -> 24
-ABI_VERSION = 8
+ABI_VERSION = 9
 FWD_AUTO, FWD_ROWS, FWD_NO_AGEMM, FWD_TILE, FWD_ROWS16, FWD_ROWS8 = 0, 1, 2, 3, 4, 5
 
 E_ARG, E_SHAPE, E_HIP, E_PLAN = -1, -2, -3, -4
@@ -101,6 +101,8 @@ SIGNATURES = {
     "dgprf_profile_step": (_i32, [ctypes.POINTER(Plan), ctypes.POINTER(Chain),
                                   ctypes.POINTER(Batch), ctypes.POINTER(Step), _i32, _vp, _vp]),
     "dgprf_forward_scratch": (_i32, [ctypes.POINTER(Plan), _i64, ctypes.POINTER(_i64)]),
+    "dgprf_forward_samples_scratch": (_i32, [ctypes.POINTER(Plan), _i64, _i32,
+                                             ctypes.POINTER(_i64)]),
     "dgprf_forward": (_i32, [ctypes.POINTER(Plan), _vp, _vp, _vp, _vp, _vp, _i32, _i64,
                              ctypes.POINTER(_vp), _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp]),
     "dgprf_lse_finalize": (_i32, [_vp, _vp, _vp, _i32, _i64, ctypes.c_double, ctypes.c_float,

@@ -598,13 +598,19 @@ class Engine:
         m, s, e = lse
         om = self.omega if omega is None else omega
         ops().forward_samples(self._plan_t(self.layout), thetas, om, self.der, X, a1, Yd, m, s, e,
-                              None if a1 is not None else self.forward_scratch(X.shape[0]))
+                              self.forward_scratch(X.shape[0], thetas.shape[0]))
 
-    def forward_scratch(self, n):
-        """Engine-owned scratch of dgprf_forward for n rows (the wide-first-layer A_1 chunks),
-        grown on demand and reused, so the predictive loop allocates nothing per sample."""
+    def forward_scratch(self, n, n_samples=0):
+        """Engine-owned scratch of dgprf_forward for n rows (the wide-first-layer A_1 chunks) or,
+        with n_samples, of dgprf_forward_samples (also every sample's per-row log p, so all sample
+        pairs run in one launch); grown on demand and reused, so the predictive loop allocates
+        nothing per sample."""
         need = ctypes.c_int64(0)
-        N.call("dgprf_forward_scratch", ctypes.byref(self.layout), int(n), ctypes.byref(need))
+        if n_samples:
+            N.call("dgprf_forward_samples_scratch", ctypes.byref(self.layout), int(n),
+                   int(n_samples), ctypes.byref(need))
+        else:
+            N.call("dgprf_forward_scratch", ctypes.byref(self.layout), int(n), ctypes.byref(need))
         if need.value == 0:
             return None
         if self._fwd_scratch is None or self._fwd_scratch.numel() < need.value:

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define DGPRF_ABI_VERSION 8
+#define DGPRF_ABI_VERSION 9
 
 #define DGPRF_MAX_LAYERS 8
 #define DGPRF_MAX_G 64        /* max latent GPs per layer (n_gp[l]) */
@@ -327,6 +327,11 @@ int dgprf_forward(const dgprf_plan_t *plan, const float *theta, const float *ome
  * dgprf_forward calls would.  Lean models (every layer d, g <= 8, n large enough for the tile
  * kernel) score two samples per pass with layer 0 computed once for the pair (Omega is fixed across
  * samples, layers/rf_layers.py:21-22); other models run one forward per sample.  ABI 8. */
+/* Floats of device scratch that let dgprf_forward_samples score n_samples samples of n rows in its
+ * fastest form (every sample pair in one launch, then a fold in sample order; at least the
+ * dgprf_forward_scratch figure).  Less scratch still works: one launch per pair.  Host-only.  ABI 9. */
+int dgprf_forward_samples_scratch(const dgprf_plan_t *plan, int64_t n, int32_t n_samples,
+                                  int64_t *floats_out);
 int dgprf_forward_samples(const dgprf_plan_t *plan, const float *thetas, int32_t n_samples,
                           const float *omega, const float *der, const float *X, const float *A1,
                           const float *Y, int32_t y_cols, int64_t n, float *lse_m, float *lse_s,

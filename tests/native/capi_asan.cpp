@@ -66,6 +66,10 @@ static void check_layout(const dgprf_plan_t& p) {
   for (int64_t n : {(int64_t)0, (int64_t)1, (int64_t)1000, (int64_t)100000, (int64_t)10000000}) {
     int64_t need = -1;
     CHECK(dgprf_forward_scratch(&p, n, &need) == DGPRF_OK && need >= 0);
+    for (int32_t S : {1, 2, 3, 20}) {
+      int64_t need_s = -1;
+      CHECK(dgprf_forward_samples_scratch(&p, n, S, &need_s) == DGPRF_OK && need_s >= need);
+    }
   }
 }
 
@@ -217,6 +221,10 @@ int main() {
   CHECK(dgprf_profile_step(&ok, &ch, &bt, &st, 5, nullptr, nullptr) == DGPRF_E_ARG);
   CHECK(dgprf_forward_scratch(&ok, -1, &i64) == DGPRF_E_ARG);
   CHECK(dgprf_forward_scratch(&uninit, 10, &i64) == DGPRF_E_PLAN);
+  CHECK(dgprf_forward_samples_scratch(&ok, 10, 0, &i64) == DGPRF_E_ARG);
+  CHECK(dgprf_forward_samples_scratch(&ok, -1, 2, &i64) == DGPRF_E_ARG);
+  CHECK(dgprf_forward_samples_scratch(&ok, 10, 2, nullptr) == DGPRF_E_ARG);
+  CHECK(dgprf_forward_samples_scratch(&uninit, 10, 2, &i64) == DGPRF_E_PLAN);
   CHECK(dgprf_forward(&ok, nullptr, &f, &f, &f, &f, 1, 10, nullptr, nullptr, nullptr, nullptr,
                       nullptr, nullptr, nullptr, 0, nullptr) == DGPRF_E_ARG);
   CHECK(dgprf_forward(&ok, &f, &f, &f, &f, nullptr, 1, 10, nullptr, &f, nullptr, nullptr,

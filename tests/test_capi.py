@@ -28,7 +28,7 @@ def test_exports_every_declared_symbol():
     for n in names:
         assert hasattr(lib, n), n
     assert set(names) == set(N.SIGNATURES), set(names) ^ set(N.SIGNATURES)
-    assert lib.dgprf_abi_version() == N.ABI_VERSION == 8
+    assert lib.dgprf_abi_version() == N.ABI_VERSION == 9
 
 
 def test_struct_layout_matches_c(tmp_path):

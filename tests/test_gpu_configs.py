@@ -179,6 +179,54 @@ def test_config_predictive_rows(dev, cfg):
     assert np.max(np.abs(lp - ref)) < 2e-5 * max(1.0, np.max(np.abs(ref)))
 
 
+@pytest.mark.parametrize("cfg,n_test", [(3, 4573), (4, 1000), (5, 700)])
+def test_config_predictive_samples_one_launch_bit_equal(dev, cfg, n_test):
+    """dgprf_forward_samples with the scratch of dgprf_forward_samples_scratch scores S samples in
+    ONE launch of the one-sample predictive kernel (grid.z = sample; config 4 reading the resident
+    X Omega_1), per-row log p / se to scratch, then k_lse_fold_samples in sample order; without
+    that scratch it launches once per sample and folds in the kernel.  Same bits; and the summed
+    result agrees with the oracle's log-sum-exp of the S samples per row."""
+    from dgprf import _native as N
+    from dgprf import engine as E
+    from dgprf.engine import ops
+    c = CONFIGS[cfg]
+    m, p = _model(c, 50 + cfg)
+    eng = m._engine
+    Xt, Yt = _data(c, n_test, 300 + cfg)
+    Xd = torch.tensor(Xt, dtype=torch.float32, device=dev)
+    Yd = torch.tensor(Yt, dtype=torch.float32, device=dev)
+    E.set_seed(51)
+    S = 3
+    thetas = torch.stack([E.normal((1, eng.layout.w_total), N.RNG_W) for _ in range(S)])
+    eng.build_omega()
+    a1 = eng.dataset_a1(Xd)
+    assert (a1 is not None) == (cfg == 4)
+    scr = eng.forward_scratch(n_test, S)
+    assert scr is not None and scr.numel() >= S * n_test
+    outs = []
+    assert a1 is not None or eng.forward_scratch(n_test) is None  # no A_1 chunks needed
+    for sc in (scr, None):
+        acc = [torch.full((1, n_test), -np.inf, device=dev), torch.zeros(1, n_test, device=dev),
+               torch.zeros(1, n_test, device=dev) if c["lik"] == "gaussian" else None]
+        ops().forward_samples(eng._plan_t(eng.layout), thetas, eng.omega, eng.der, Xd, a1, Yd,
+                              acc[0], acc[1], acc[2], sc)
+        torch.cuda.synchronize()
+        outs.append([cpu(a) for a in acc if a is not None])
+    for a, b in zip(outs[0], outs[1]):
+        assert np.array_equal(a, b), cfg
+    lps = []
+    for j in range(S):
+        W = unpack(eng, thetas[j])
+        pj = O.Params(p.d_in, p.d_out, p.n_rf, p.n_gp, p.kinds, p.likelihood, False, z=p.z, W=W,
+                      log_inv_ls=p.log_inv_ls, lik_log_var=p.lik_log_var)
+        lps.append(O.log_prob(pj, O.forward(pj, Xt), Yt))
+    lps = np.stack(lps)
+    mx = lps.max(axis=0)
+    ref = mx + np.log(np.exp(lps - mx).sum(axis=0))
+    got = outs[0][0][0] + np.log(outs[0][1][0])
+    assert np.max(np.abs(got - ref)) < 2e-5 * max(1.0, np.max(np.abs(ref))), cfg
+
+
 @pytest.mark.parametrize("cfg", [3, 4, 5])
 def test_config_graph_steps_finite_and_deterministic(dev, cfg):
     """200 graph-replayed steps with on-device minibatches of B = 200 at the config's N (config 5

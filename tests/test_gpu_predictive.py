@@ -148,6 +148,39 @@ def test_predictive_two_samples_per_launch(dev, C, S):
     assert abs(ll - ref_ll) < 1e-4 and abs(rmse - ref_rmse) < 1e-5 * ref_rmse
 
 
+@pytest.mark.parametrize("C,S", [(1, 5), (2, 4)])
+def test_predictive_pairs_one_launch_equals_launch_per_pair(dev, C, S):
+    """dgprf_forward_samples with the scratch of dgprf_forward_samples_scratch runs every sample pair
+    in ONE launch (grid.z = pair), writes each sample's per-row log p / squared error to scratch
+    and folds them in sample order with k_lse_fold_samples; without that scratch it launches the
+    pair kernel once per pair and folds in place.  Both must give the same bits."""
+    from dgprf import _native as N
+    from dgprf import engine as E
+    from dgprf.data import regression_data
+    from dgprf.engine import ops
+    n_test = 20_001  # the pair kernel applies from 16,384 rows (the lean tile kernel's range)
+    Xt, Yt, _ = regression_data(n_test, CFG2["D"], seed=17, device=dev)
+    m = _config2_model(21)
+    eng = m._engine if C == 1 else _multi_chain_engine(m, C, seed=79)
+    eng.build_omega()
+    E.set_seed(22)
+    thetas = torch.stack([E.normal((C, eng.layout.w_total), N.RNG_W) for _ in range(S)])
+    Y2 = Yt if Yt.dim() == 2 else Yt[:, None]
+    need = eng.forward_scratch(n_test, S)
+    assert need is not None and need.numel() >= 2 * S * C * n_test
+    outs = []
+    for scr in (need, None):
+        acc = [torch.full((C, n_test), -np.inf, device=dev), torch.zeros(C, n_test, device=dev),
+               torch.zeros(C, n_test, device=dev)]
+        ops().forward_samples(eng._plan_t(eng.layout), thetas, eng.omega, eng.der, Xt, None, Y2,
+                              acc[0], acc[1], acc[2], scr)
+        torch.cuda.synchronize()
+        outs.append([cpu(a) for a in acc])
+    for a, b in zip(outs[0], outs[1]):
+        assert np.array_equal(a, b)
+    assert np.isfinite(outs[0][0]).all() and (outs[0][1] > 0).all()
+
+
 def _multi_chain_engine(m, C, seed):
     """C chains sharing model m's frequencies and hyper-parameters (one posterior)."""
     from dgprf import engine as E
