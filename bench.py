@@ -436,7 +436,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10000)
     ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--steps-per-graph", type=int, default=100)
-    ap.add_argument("--pred-samples", type=int, default=20)
+    ap.add_argument("--pred-samples", type=int, default=40)
     ap.add_argument("--multi-chains", type=int, default=64)
     ap.add_argument("--full-bayes-steps", type=int, default=2000)
     ap.add_argument("--cpu-runs", type=int, default=5)

@@ -324,9 +324,13 @@ int dgprf_forward(const dgprf_plan_t *plan, const float *theta, const float *ome
  * samples, experiments/utils_training.py:79-85): thetas [n_samples][n_chains][w_total]; each
  * sample's per-row log p (and squared error) is folded into the chain's online log-sum-exp
  * accumulators lse_m / lse_s (and se_sum, Gaussian) [n_chains][n] in sample order, as n_samples
- * dgprf_forward calls would.  Lean models (every layer d, g <= 8, n large enough for the tile
- * kernel) score two samples per pass with layer 0 computed once for the pair (Omega is fixed across
- * samples, layers/rf_layers.py:21-22); other models run one forward per sample.  ABI 8. */
+ * dgprf_forward calls would (the same bits).  Lean models (every layer d, g <= 8, n large enough
+ * for the tile kernel) score two samples per pass with layer 0 computed once for the pair (Omega
+ * is fixed across samples, layers/rf_layers.py:21-22); other models run the one-sample kernels.
+ * With scratch_floats >= dgprf_forward_samples_scratch every sample (pair) runs in ONE launch and
+ * scratch receives the per-row log p / squared errors [n_samples][n_chains][n] that a fold kernel
+ * then applies in sample order; with less, one launch per sample (pair) folds in place.  ABI 8;
+ * the one-launch form ABI 9. */
 /* Floats of device scratch that let dgprf_forward_samples score n_samples samples of n rows in its
  * fastest form (every sample pair in one launch, then a fold in sample order; at least the
  * dgprf_forward_scratch figure).  Less scratch still works: one launch per pair.  Host-only.  ABI 9. */
