@@ -45,6 +45,62 @@ def as_device(x, dev, dtype=_F32):
     return x.to(device=dev, dtype=dtype).contiguous()
 
 
+class HostStage:
+    """Per-call host batches (numpy, or CPU tensors) -> device, as the reference's driver loop
+    feeds them (experiments/utils_training.py:45-61): X and Y are packed into one slot of a ring
+    of pinned host buffers and sent with ONE asynchronous H2D copy into the matching device slot,
+    instead of two pageable copies that each block the host until the GPU drained the previous
+    step.  A pinned slot is rewritten only after its copy completed (an event per slot); a device
+    slot is rewritten by a copy stream-ordered after the step that read it."""
+    SLOTS = 4
+
+    def __init__(self, dev):
+        self.dev = dev
+        self.cap = 0
+        self.k = 0
+
+    def _grow(self, n):
+        self.cap = max(int(n), 2 * self.cap, 4096)
+        self.host = [torch.empty(self.cap, dtype=_F32, pin_memory=True) for _ in range(self.SLOTS)]
+        self.host_np = [h.numpy() for h in self.host]
+        self.devb = [torch.empty(self.cap, dtype=_F32, device=self.dev) for _ in range(self.SLOTS)]
+        self.ev = [torch.cuda.Event() for _ in range(self.SLOTS)]
+        self.used = [False] * self.SLOTS
+        self.views = {}  # (slot, X shape, Y shape) -> host / device views of that slot
+
+    def _views(self, i, xs, ys):
+        key = (i, xs, ys)
+        v = self.views.get(key)
+        if v is None:
+            nx, ny = math.prod(xs), math.prod(ys)
+            h, d = self.host_np[i], self.devb[i]
+            v = (h[:nx].reshape(xs), h[nx:nx + ny].reshape(ys), self.host[i][:nx + ny],
+                 d[:nx + ny], d[:nx].view(xs), d[nx:nx + ny].view(ys))
+            self.views[key] = v
+        return v
+
+    def put(self, X, Y):
+        Xn = X.numpy() if torch.is_tensor(X) else np.asarray(X)
+        Yn = Y.numpy() if torch.is_tensor(Y) else np.asarray(Y)
+        if Xn.ndim != 2:
+            raise ValueError(f"X must be 2-D, got shape {Xn.shape}")
+        if Xn.size + Yn.size > self.cap:
+            if self.cap:
+                torch.cuda.synchronize(self.dev)  # the old slots may still be in flight
+            self._grow(Xn.size + Yn.size)
+        i = self.k % self.SLOTS
+        self.k += 1
+        if self.used[i]:
+            self.ev[i].synchronize()
+        hx, hy, hs, ds, dx, dy = self._views(i, Xn.shape, Yn.shape)
+        np.copyto(hx, Xn, casting="unsafe")
+        np.copyto(hy, Yn, casting="unsafe")
+        ds.copy_(hs, non_blocking=True)
+        self.ev[i].record()
+        self.used[i] = True
+        return dx, dy
+
+
 def ops():
     """torch.ops.dgprf — the hot-path entry points registered with torch's dispatcher
     (libdgprf_torch.so over the C-ABI).  Raises if the extension is not built."""
@@ -163,6 +219,7 @@ class Engine:
         self.resident_a1 = True
         self.hyper_epoch = 0
         self._a1_cache = {}
+        self._stage = None  # HostStage for per-call host batches
 
     # ---------------------------------------------------------------- views
     def W_view(self, l, chain=0):
@@ -400,9 +457,17 @@ class Engine:
         return self._a1_cache[key][0]
 
     # ---------------------------------------------------------------- hot path
-    def _prep_batch(self, X, Y):
-        X = as_device(X, self.dev)
-        Y = as_device(Y, self.dev)
+    def _prep_batch(self, X, Y, stage=False):
+        """stage: X, Y are one call's batch (never a dataset a graph keeps): host arrays go through
+        the pinned HostStage ring"""
+        host = lambda t: not torch.is_tensor(t) or t.device.type == "cpu"
+        if stage and host(X) and host(Y) and self.dev.type == "cuda":
+            if self._stage is None:
+                self._stage = HostStage(self.dev)
+            X, Y = self._stage.put(X, Y)
+        else:
+            X = as_device(X, self.dev)
+            Y = as_device(Y, self.dev)
         if X.dim() != 2 or X.shape[1] != self.spec.d_in:
             raise ValueError(f"X must be [B, {self.spec.d_in}], got {tuple(X.shape)}")
         if Y.dim() == 1:
@@ -438,7 +503,7 @@ class Engine:
         return t[1]
 
     def _op_batch(self, X, Y, batch_size, mode, idx, perm_seed, full_bayes=False):
-        X, Y = self._prep_batch(X, Y)
+        X, Y = self._prep_batch(X, Y, stage=mode == N.BATCH_DIRECT)
         B = X.shape[0] if mode == N.BATCH_DIRECT else int(batch_size)
         pl, ws = self.plan_ws(B, full_bayes=full_bayes)
         if idx is not None:

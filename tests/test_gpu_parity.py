@@ -373,6 +373,36 @@ def test_per_call_sgmcmc_update_equals_graph_replays(dev):
     assert len(calls) == n0 + 1
 
 
+def test_per_call_host_batches_equal_device_batches(dev):
+    """Host minibatches (float32 / float64 numpy, CPU tensors, 1-D Y) go through the pinned
+    HostStage ring (one async H2D copy per call); 14 calls — past the ring's 4 slots, with a
+    larger batch mid-run that regrows it — are bit-equal to the same calls on device batches."""
+    from likelihoods import Gaussian
+    from models.regression_model import RegressionDGP
+    from dgprf import engine as E
+    E.set_seed(23)
+    a = RegressionDGP(8, 1, n_hidden_layers=2, n_rf=64, n_gp=[8, 1], likelihood=Gaussian())
+    E.set_seed(23)
+    b = RegressionDGP(8, 1, n_hidden_layers=2, n_rf=64, n_gp=[8, 1], likelihood=Gaussian())
+    n = 4000
+    for mm in (a, b):
+        mm.precond_update(None, n, precond_type="identity")
+    b._engine.mom.copy_(a._engine.mom)
+    g = torch.Generator().manual_seed(4)
+    for t in range(14):
+        B = 600 if t == 7 else 200
+        Xh = torch.randn(B, 8, generator=g)
+        Yh = torch.randn(B, generator=g)
+        a.sgmcmc_update(Xh.to(dev), Yh.to(dev), n, lr=0.01, momentum_decay=0.9)
+        form = t % 3
+        xh = Xh.numpy() if form == 0 else (Xh.double().numpy() if form == 1 else Xh)
+        yh = Yh.numpy() if form != 2 else Yh
+        b.sgmcmc_update(xh, yh, n, lr=0.01, momentum_decay=0.9)
+    assert b._engine._stage is not None and b._engine._stage.k == 14
+    assert torch.equal(a._engine.theta, b._engine.theta)
+    assert torch.equal(a._engine.mom, b._engine.mom)
+
+
 def test_checkpoint_resume_bit_exact(dev, tmp_path):
     """save() at step 100 -> load() into a freshly built model -> 100 more graph-replayed steps is
     bitwise the 200 uninterrupted steps (SURVEY §5 checkpoint / resume; the reference keeps only
