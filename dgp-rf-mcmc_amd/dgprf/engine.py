@@ -50,8 +50,9 @@ class HostStage:
     feeds them (experiments/utils_training.py:45-61): X and Y are packed into one slot of a ring
     of pinned host buffers and sent with ONE asynchronous H2D copy into the matching device slot,
     instead of two pageable copies that each block the host until the GPU drained the previous
-    step.  A pinned slot is rewritten only after its copy completed (an event per slot); a device
-    slot is rewritten by a copy stream-ordered after the step that read it."""
+    step.  A slot (pinned and device buffer) is rewritten only after the event recorded behind
+    the op that read it completed (release(); behind the copy if no op followed), so the ring is
+    safe when calls alternate streams too."""
     SLOTS = 4
 
     def __init__(self, dev):
@@ -98,7 +99,12 @@ class HostStage:
         ds.copy_(hs, non_blocking=True)
         self.ev[i].record()
         self.used[i] = True
+        self.last = i
         return dx, dy
+
+    def release(self):
+        """After the op that read the last slot was enqueued: its event now covers that op."""
+        self.ev[self.last].record()
 
 
 def ops():
@@ -220,6 +226,7 @@ class Engine:
         self.hyper_epoch = 0
         self._a1_cache = {}
         self._stage = None  # HostStage for per-call host batches
+        self._staged = False  # the current op's batch came through it (release after the op)
 
     # ---------------------------------------------------------------- views
     def W_view(self, l, chain=0):
@@ -465,6 +472,7 @@ class Engine:
             if self._stage is None:
                 self._stage = HostStage(self.dev)
             X, Y = self._stage.put(X, Y)
+            self._staged = True
         else:
             X = as_device(X, self.dev)
             Y = as_device(Y, self.dev)
@@ -531,6 +539,7 @@ class Engine:
             idx, float(lr), float(beta), float(T), float(data_size), bool(resample), dv(xi),
             dv(xi_resample), bool(full_bayes), self.z if z is None else z, self.hyp, self.hmom,
             self.hmass, dv(xi_hyp), dv(xi_hyp_resample))
+        self._release_stage()
 
     def grad(self, X, Y, data_size, build=True, omega=None, batch_size=None,
              mode=N.BATCH_DIRECT, idx=None, perm_seed=0, full_bayes=False, z=None):
@@ -542,10 +551,17 @@ class Engine:
                                                       full_bayes)
         if build:
             self.build_omega()
-        return ops().potential_grad(
+        g = ops().potential_grad(
             self._plan_t(pl), self.theta, self.omega if omega is None else omega, self.der,
             self.mass, ws, self.step_ctr, X, Y, int(mode), iters, ps, idx, float(data_size),
             bool(full_bayes), self.z if z is None else z, self.hyp, self.hmom, self.hmass)
+        self._release_stage()
+        return g
+
+    def _release_stage(self):
+        if self._staged:
+            self._staged = False
+            self._stage.release()
 
     def graph(self, X_all, Y_all, batch_size, data_size, lr, beta, T, steps_per_graph,
               schedule=N.SCHED_CONST, start_step=0, cycle_length=1, resample_head=False,
