@@ -80,9 +80,15 @@ class HostStage:
             self.views[key] = v
         return v
 
+    @staticmethod
+    def _host_array(t):
+        if not torch.is_tensor(t):
+            return np.asarray(t)
+        t = t.detach()
+        return (t.float() if t.dtype == torch.bfloat16 else t).numpy()
+
     def put(self, X, Y):
-        Xn = X.numpy() if torch.is_tensor(X) else np.asarray(X)
-        Yn = Y.numpy() if torch.is_tensor(Y) else np.asarray(Y)
+        Xn, Yn = self._host_array(X), self._host_array(Y)
         if Xn.ndim != 2:
             raise ValueError(f"X must be 2-D, got shape {Xn.shape}")
         if Xn.size + Yn.size > self.cap:

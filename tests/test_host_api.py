@@ -77,3 +77,15 @@ def test_utils():
     assert np.allclose(lp.cpu().numpy(), 2 * (-0.5 * (np.log(2 * np.pi) + np.log(0.5) + 2.0)))
     sm = Softmax().log_prob(torch.tensor([[0.0, 1.0]]), torch.tensor([[1.0]]))
     assert np.isclose(float(sm), 1.0 - np.log(1 + np.e))
+
+
+def test_host_stage_array_forms():
+    """Per-call host batches accepted by the pinned staging ring (dgprf.engine.HostStage): numpy
+    arrays, lists, CPU tensors that track gradients, bf16 CPU tensors (cast to fp32 on the host)."""
+    from dgprf.engine import HostStage
+    a = HostStage._host_array(torch.ones(2, 3, dtype=torch.bfloat16, requires_grad=True))
+    assert a.dtype == np.float32 and a.shape == (2, 3)
+    assert HostStage._host_array([[1.0, 2.0]]).shape == (1, 2)
+    x = np.arange(6, dtype=np.float64).reshape(3, 2)
+    assert HostStage._host_array(x) is x
+    assert HostStage._host_array(torch.zeros(4)).dtype == np.float32
