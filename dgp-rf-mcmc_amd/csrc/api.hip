@@ -207,9 +207,15 @@ int dgprf_plan_init(dgprf_plan_t* pl) {
     om = align4(om + (int64_t)pl->d[l] * pl->n_rf[l]);
     pl->w_off[l] = w;
     w = align4(w + (int64_t)pl->P[l] * pl->n_gp[l]);
-    // step decomposition: <= 16 feature slices of 4 waves x cpw 16-feature chunks
+    // step decomposition: <= 16 feature slices of 4 waves x cpw 16-feature chunks.  Several
+    // chains per launch fill the chip with chains, and wider slices then cut the per-slice partial
+    // round trips: >= 4 chunks per wave from 4 chains, >= 8 from 16 (config 2, chain-steps/s at
+    // 4 / 8 / 16 / 64 chains: 91.6k / 118k / 144k / 170k with 16 slices, 103k / 156k / 209k / 276k
+    // with 4, 82k / 150k / 217k / 280k with 2; 2 chains: 16 slices best)
     const int chunks = (pl->n_rf[l] + 15) / 16;
-    const int cpw = (chunks + 4 * 16 - 1) / (4 * 16);
+    int cpw = (chunks + 4 * 16 - 1) / (4 * 16);
+    const int cmin = pl->n_chains >= 16 ? 8 : (pl->n_chains >= 4 ? 4 : 1);
+    cpw = std::max(cpw, std::min(cmin, (chunks + 3) / 4));
     pl->cpw[l] = cpw < 1 ? 1 : cpw;
     pl->ns[l] = (chunks + 4 * pl->cpw[l] - 1) / (4 * pl->cpw[l]);
   }

@@ -95,6 +95,48 @@ def test_config_forward_and_grad(dev, cfg):
         assert rel_err(G[l], ref[l]) < 2e-4, (cfg, l)
 
 
+@pytest.mark.parametrize("C", [4, 16])
+@pytest.mark.parametrize("cfg", [2, 3, 4, 5])
+def test_multichain_wide_slices_grad(dev, cfg, C):
+    """From 4 / 16 chains per launch the plan takes wider feature slices than one chain (>= 4 / 8
+    16-feature chunks per wave, dgprf_plan_init): chain 0 (the one-chain model's W) gives the
+    one-chain gradient to float tolerance (another summation order), and the last chain (its W
+    scaled) matches the float64 oracle."""
+    import copy
+    from dgprf import engine as E
+    c = CONFIGS[cfg]
+    L = len(c["kinds"])
+    m, p = _model(c, 30 + cfg)
+    X, Y = _data(c, 2 * c["B"], cfg)
+    X, Y = _rows_off_kinks(c, p, X, Y, c["B"])
+    N_ = {2: 1_000_000, 3: 45_730, 4: 60_000, 5: 10_000_000}[cfg]
+    one = m._engine
+    mc = E.Engine(one.spec, C, seed=one.seed)
+    chunks = [(r + 15) // 16 for r in c["n_rf"]]
+    want = [max((k + 63) // 64, min(8 if C >= 16 else 4, (k + 3) // 4)) for k in chunks]
+    assert list(mc.layout.cpw[:L]) == want
+    mc.z.copy_(one.z)
+    mc.hyp.copy_(one.hyp)
+    mc.lik_log_var_source = one.lik_log_var_source
+    s_last = 1.0 + 0.05 * (C - 1)
+    scale = 1.0 + 0.05 * torch.arange(C, device=dev, dtype=torch.float32)[:, None]
+    mc.theta.copy_(one.theta[:1] * scale)
+    mc.init_moments()
+    mc.build_omega()
+    Xd = torch.as_tensor(X, dtype=torch.float32, device=dev)
+    Yd = torch.as_tensor(Y, dtype=torch.float32, device=dev)
+    G1 = one.grad(Xd, Yd, N_)
+    G = mc.grad(Xd, Yd, N_)
+    assert torch.isfinite(G).all()
+    assert rel_err(cpu(G[0]), cpu(G1[0])) < 2e-5
+    pc = copy.copy(p)
+    pc.W = [w * np.float64(np.float32(s_last)) for w in p.W]
+    ref = O.grad_W(pc, X, Y, N_)
+    Gl = unpack(mc, G, chain=C - 1)
+    for l in range(L):
+        assert rel_err(Gl[l], ref[l]) < 2e-4, (cfg, C, l)
+
+
 @pytest.mark.parametrize("cfg", [2, 3])
 @pytest.mark.parametrize("path", ["tile", "rows16", "rows8", "rows"])
 def test_predictive_paths_small_test_set(dev, path, cfg):

@@ -425,6 +425,30 @@ def test_full_bayes_per_chain_hyper_parameters(dev):
         assert rel_err(cpu(F[c]), O.forward(ps[c], X)) < 2e-5, c
 
 
+@pytest.mark.parametrize("C", [4, 16])
+def test_full_bayes_per_chain_wide_slices(dev, C):
+    """Per-chain hyper-parameters with 4 / 16 chains, whose plans take wider feature slices
+    (4 / 8 16-feature chunks per wave at n_rf = 1024): the full-Bayes gradient of the first and
+    last chain matches the oracle at that chain's state."""
+    spec_args = (3, 1, ["RBF", "ARC"], [1024, 512], [4, 1], False, "gaussian")
+    ard, flags = [0, 1], ("kernel", "lik", "mean")
+    rng = np.random.default_rng(310 + C)
+    eng = engine_for(spec_args, ard, flags, C=C)
+    assert eng.layout.cpw[0] == (8 if C >= 16 else 4)
+    ps = [random_params(rng, spec_args, ard) for _ in range(C)]
+    for c in range(1, C):
+        ps[c].z = ps[0].z
+    for c in range(C):
+        load_chain(eng, ps[c], c)
+    tr = O.Trainable(kernel=True, lik=True, mean=True, ard=[bool(a) for a in ard])
+    B, N_ = 64, 3000
+    X = rng.standard_normal((B, spec_args[0]))
+    Y = rng.standard_normal((B, 1))
+    G = eng.grad(X, Y, N_, full_bayes=True)
+    for c in (0, C - 1):
+        check_grad(eng, G, c, O.grad_full(ps[c], X, Y, N_, tr), tr)
+
+
 def test_full_bayes_config4_shape_large_batch(dev):
     """full_bayesian=True at BASELINE config 4's model shape (784-wide first layer, 4 x RBF n_rf
     4096, g [30,30,30,10], softmax) with B = 600: the W-only row-group layout fits, the full-Bayes
