@@ -73,6 +73,8 @@ class HostStage:
         key = (i, xs, ys)
         v = self.views.get(key)
         if v is None:
+            if len(self.views) >= 64:  # many distinct batch shapes: start over
+                self.views.clear()
             nx, ny = math.prod(xs), math.prod(ys)
             h, d = self.host_np[i], self.devb[i]
             v = (h[:nx].reshape(xs), h[nx:nx + ny].reshape(ys), self.host[i][:nx + ny],
