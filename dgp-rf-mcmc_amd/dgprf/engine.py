@@ -104,15 +104,15 @@ class HostStage:
         hx, hy, hs, ds, dx, dy = self._views(i, Xn.shape, Yn.shape)
         np.copyto(hx, Xn, casting="unsafe")
         np.copyto(hy, Yn, casting="unsafe")
-        ds.copy_(hs, non_blocking=True)
-        self.ev[i].record()
+        ds.copy_(hs, non_blocking=True)  # on the device's current stream, like the op
+        self.ev[i].record(torch.cuda.current_stream(self.dev))
         self.used[i] = True
         self.last = i
         return dx, dy
 
     def release(self):
         """After the op that read the last slot was enqueued: its event now covers that op."""
-        self.ev[self.last].record()
+        self.ev[self.last].record(torch.cuda.current_stream(self.dev))
 
 
 def ops():
