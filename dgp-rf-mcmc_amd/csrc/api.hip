@@ -118,7 +118,8 @@ int check_step(const dgprf_step_t* st) {
 // replays, where the next step is known to follow).  The update kernel sums the gW partials and
 // updates every W (and the full-Bayes hyper-parameters).
 hipError_t enqueue_step(const dgprf_plan_t& pl, const StepDev& sd_in, const UpdateDev& ud,
-                        hipStream_t s, bool prep_gather = true, bool gather_next = false) {
+                        hipStream_t s, bool prep_gather = true, bool gather_next = false,
+                        bool advance = false) {
   hipError_t e = hipSuccess;
   StepDev sd = sd_in;
   if (sd.full_bayes) sd.bd.A1 = nullptr;  // Omega_1 changes every full-Bayes step: the GEMM
@@ -132,7 +133,7 @@ hipError_t enqueue_step(const dgprf_plan_t& pl, const StepDev& sd_in, const Upda
   }
   for (int l = pl.n_layers - 1; l >= 0 && e == hipSuccess; --l)
     e = dgprf::launch_step_bwd(pl, sd, l, s);
-  if (e == hipSuccess) e = dgprf::launch_step_update(pl, sd, ud, nullptr, s, gather_next);
+  if (e == hipSuccess) e = dgprf::launch_step_update(pl, sd, ud, nullptr, s, gather_next, advance);
   return e;
 }
 
@@ -280,8 +281,10 @@ int dgprf_plan_init(dgprf_plan_t* pl) {
     pl->hpp_off[l] = ws;
     ws = align4(ws + (int64_t)pl->n_rt_pad * DGPRF_NS_MAX * align4(2 * pl->d[l] + 1));
   }
-  pl->hpl_off = ws;  // then DGPRF_MAX_LAYERS uint32 arrival counters of the hyper workgroups
-  ws = align4(ws + pl->n_rt_pad + DGPRF_MAX_LAYERS);
+  // then DGPRF_MAX_LAYERS uint32 arrival counters of the hyper workgroups and the eager steps'
+  // step-advance counter (dgprf_sghmc_step)
+  pl->hpl_off = ws;
+  ws = align4(ws + pl->n_rt_pad + DGPRF_MAX_LAYERS + 1);
   pl->yb_cols = pl->likelihood == DGPRF_LIK_SOFTMAX ? 1 : pl->n_gp[L - 1];
   pl->xb_off = ws;
   ws = align4(ws + (int64_t)B * pl->d_in);
@@ -336,9 +339,8 @@ int dgprf_sghmc_step(const dgprf_plan_t* plan, const dgprf_chain_t* chain,
   StepDev sd = make_step_dev(*plan, *chain, *batch, st.step_offset);
   sd.full_bayes = st.full_bayes != 0;
   const UpdateDev ud = make_update_dev(st);
-  hipError_t e = enqueue_step(*plan, sd, ud, as_stream(stream));
-  if (e == hipSuccess) e = dgprf::launch_advance(chain->step, 1, as_stream(stream));
-  return hip_rc(e);
+  // the update kernel's last workgroup advances the step counter (one launch fewer per call)
+  return hip_rc(enqueue_step(*plan, sd, ud, as_stream(stream), true, false, true));
 }
 
 int dgprf_potential_grad(const dgprf_plan_t* plan, const dgprf_chain_t* chain,

@@ -97,7 +97,8 @@ hipError_t launch_step_fwd_fused(const dgprf_plan_t& pl, const StepDev& sd, hipS
 // Sums the gW partials, adds the prior term and applies the SGHMC update (or writes the gradient);
 // gather_next: extra workgroups gather step t+1's minibatch rows.
 hipError_t launch_step_update(const dgprf_plan_t& pl, const StepDev& sd, const UpdateDev& ud,
-                              const float* grad_in, hipStream_t s, bool gather_next = false);
+                              const float* grad_in, hipStream_t s, bool gather_next = false,
+                              bool advance = false);
 // (sd.full_bayes: the same launch also runs the hyper-parameter workgroups — their gradients or
 // update and the Omega, c, sigma^2 rebuild)
 

@@ -177,6 +177,9 @@ struct UpdK {
   // full_bayesian=True: the first hyp_blocks workgroups do the hyper-parameter work
   int32_t hyp_blocks, pad_h;
   HypK hk;
+  // eager steps: arrival counter of the workgroups, the last one advancing *step (else null)
+  unsigned* adv_cnt;
+  int64_t* step_adv;
 };
 
 // v if ok else 0, written so that the compiler cannot sink the (always in-range, finite) load

@@ -366,8 +366,7 @@ __device__ void hyper_block(const UpdK& a, int hb, int chain, float* sm, int sb)
 }
 
 template <bool GIN, bool GONLY, bool XI, bool CYC>
-__global__ __launch_bounds__(UPD_THREADS) void k_step_update(const UpdK a) {
-  extern __shared__ __attribute__((aligned(16))) float usm[];
+__device__ __forceinline__ void update_block(const UpdK& a, float* usm) {
   const int chain = blockIdx.y;
   const int stamp_base = 16 * 4096 + blockIdx.y * gridDim.x + blockIdx.x;
   DGPRF_STAMP(stamp_base, 0);
@@ -405,6 +404,25 @@ __global__ __launch_bounds__(UPD_THREADS) void k_step_update(const UpdK a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
   DGPRF_STAMP(stamp_base, 14);
+}
+
+template <bool GIN, bool GONLY, bool XI, bool CYC>
+__global__ __launch_bounds__(UPD_THREADS) void k_step_update(const UpdK a) {
+  extern __shared__ __attribute__((aligned(16))) float usm[];
+  update_block<GIN, GONLY, XI, CYC>(a, usm);
+  // eager steps (adv_cnt set): the last workgroup to finish advances the step counter — the
+  // launch of k_advance a graph makes once per replay.  Every workgroup has consumed its read of
+  // the counter before it arrives, so none of them sees the new value.
+  if (a.adv_cnt) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned total = gridDim.x * gridDim.y;
+      if (atomicAdd(a.adv_cnt, 1u) == total - 1u) {
+        atomicExch(a.adv_cnt, 0u);
+        atomicAdd(reinterpret_cast<unsigned long long*>(a.step_adv), 1ull);
+      }
+    }
+  }
 }
 
 
@@ -745,7 +763,8 @@ hipError_t launch_step_bwd(const dgprf_plan_t& pl, const StepDev& sd, int layer,
 }
 
 hipError_t launch_step_update(const dgprf_plan_t& pl, const StepDev& sd, const UpdateDev& ud,
-                              const float* grad_in, hipStream_t s, bool gather_next) {
+                              const float* grad_in, hipStream_t s, bool gather_next,
+                              bool advance) {
   if (pl.w_total >= (int64_t)1 << 30 || (int64_t)pl.n_rt_pad * pl.w_total >= (int64_t)1 << 29)
     return hipErrorInvalidValue;  // 32-bit buffer offsets
   UpdK a;
@@ -772,6 +791,12 @@ hipError_t launch_step_update(const dgprf_plan_t& pl, const StepDev& sd, const U
   a.e_end = a.hi[pl.n_layers - 1];
   a.pad_e = 0;
   a.gather_next = gather_next && sd.bd.mode == DGPRF_BATCH_EPOCH ? 1 : 0;
+  // the step-advance arrival counter after the hyper workgroups' counters (chain 0's workspace)
+  a.adv_cnt = advance && sd.ws ? reinterpret_cast<unsigned*>(sd.ws + pl.hpl_off + pl.n_rt_pad +
+                                                              DGPRF_MAX_LAYERS)
+                               : nullptr;
+  a.step_adv = const_cast<int64_t*>(sd.step);
+  if (advance && !a.adv_cnt) return hipErrorInvalidValue;
   a.B = pl.batch;
   a.d_in = pl.d_in;
   a.yb_cols = pl.yb_cols;

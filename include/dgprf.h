@@ -165,7 +165,8 @@ typedef struct dgprf_plan {
   int64_t ws_total;
   int64_t hpp_off[DGPRF_MAX_LAYERS]; /* full-Bayes partials [n_rt_pad][16][align4(2 d_l + 1)] (per chain) */
   int64_t hpl_off;                   /* full-Bayes lik_log_var partials [n_rt_pad], then 8 uint32
-                                        arrival counters of the hyper workgroups (per chain)   */
+                                        arrival counters of the hyper workgroups (per chain)
+                                        and the eager step-advance counter (chain 0)          */
   int64_t xb_off;                    /* gathered minibatch rows X [B][d_in] (per chain)        */
   int64_t yb_off;                    /* gathered minibatch targets [B][yb_cols] (per chain)    */
   int32_t yb_cols;                   /* g_L (Gaussian) or 1 (softmax label)                    */

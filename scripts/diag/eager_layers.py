@@ -68,3 +68,18 @@ d = timed(lambda i: m.sgmcmc_update(xs[i], ys[i], 1_000_000, lr=0.01, momentum_d
 E.ops = real
 print(f"us per call: (a) sgmcmc_update {a:.1f}  (b) Engine.step {b:.1f}  (c) op only {c:.1f}  "
       f"(d) python layers only {d:.1f}", flush=True)
+
+# host issue time vs device time of the op-only loop: host-bound when the issue time per call
+# matches the wall time per call
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+e0.record()
+for i in range(calls):
+    op(*pre[i % 50])
+e1.record()
+t1 = time.perf_counter()
+torch.cuda.synchronize()
+t2 = time.perf_counter()
+print(f"op-only: host issue {(t1 - t0) * 1e6 / calls:.1f} us/call, wall {(t2 - t0) * 1e6 / calls:.1f}, "
+      f"device (events) {e0.elapsed_time(e1) * 1e3 / calls:.1f}", flush=True)
