@@ -210,12 +210,15 @@ int dgprf_plan_init(dgprf_plan_t* pl) {
     w = align4(w + (int64_t)pl->P[l] * pl->n_gp[l]);
     // step decomposition: <= 16 feature slices of 4 waves x cpw 16-feature chunks.  Several
     // chains per launch fill the chip with chains, and wider slices then cut the per-slice partial
-    // round trips: >= 4 chunks per wave from 4 chains, >= 8 from 16 (config 2, chain-steps/s at
-    // 4 / 8 / 16 / 64 chains: 91.6k / 118k / 144k / 170k with 16 slices, 103k / 156k / 209k / 276k
-    // with 4, 82k / 150k / 217k / 280k with 2; 2 chains: 16 slices best)
+    // round trips: >= 4 chunks per wave from 4 chains, >= 8 from 16 when g_l <= 16 (config 2,
+    // chain-steps/s at 4 / 8 / 16 / 64 chains: 91.6k / 118k / 144k / 170k with 16 slices, 103k /
+    // 156k / 209k / 276k with 4, 82k / 150k / 217k / 280k with 2; 2 chains: 16 slices best.
+    // Config 3 at 4 / 16 / 64 chains 65k / 94k / 109k -> 87k / 141k / 169k.  Config 4's g = 30
+    // layers at 8 chunks per wave: 14.0k -> 11.8k (their whole-slice W / Omega image no longer
+    // fits the LDS), hence the g_l bound)
     const int chunks = (pl->n_rf[l] + 15) / 16;
     int cpw = (chunks + 4 * 16 - 1) / (4 * 16);
-    const int cmin = pl->n_chains >= 16 ? 8 : (pl->n_chains >= 4 ? 4 : 1);
+    const int cmin = pl->n_chains >= 16 && pl->n_gp[l] <= 16 ? 8 : (pl->n_chains >= 4 ? 4 : 1);
     cpw = std::max(cpw, std::min(cmin, (chunks + 3) / 4));
     pl->cpw[l] = cpw < 1 ? 1 : cpw;
     pl->ns[l] = (chunks + 4 * pl->cpw[l] - 1) / (4 * pl->cpw[l]);

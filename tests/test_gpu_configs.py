@@ -113,7 +113,8 @@ def test_multichain_wide_slices_grad(dev, cfg, C):
     one = m._engine
     mc = E.Engine(one.spec, C, seed=one.seed)
     chunks = [(r + 15) // 16 for r in c["n_rf"]]
-    want = [max((k + 63) // 64, min(8 if C >= 16 else 4, (k + 3) // 4)) for k in chunks]
+    want = [max((k + 63) // 64, min(8 if C >= 16 and g <= 16 else 4, (k + 3) // 4))
+            for k, g in zip(chunks, c["n_gp"])]
     assert list(mc.layout.cpw[:L]) == want
     mc.z.copy_(one.z)
     mc.hyp.copy_(one.hyp)
