@@ -83,3 +83,22 @@ torch.cuda.synchronize()
 t2 = time.perf_counter()
 print(f"op-only: host issue {(t1 - t0) * 1e6 / calls:.1f} us/call, wall {(t2 - t0) * 1e6 / calls:.1f}, "
       f"device (events) {e0.elapsed_time(e1) * 1e3 / calls:.1f}", flush=True)
+
+# the same op-only loop on a non-default stream (torch's default stream is HIP's null stream)
+side = torch.cuda.Stream()
+side.wait_stream(torch.cuda.current_stream())
+with torch.cuda.stream(side):
+    for i in range(50):
+        op(*pre[i % 50])
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e0.record()
+    for i in range(calls):
+        op(*pre[i % 50])
+    e1.record()
+    t1 = time.perf_counter()
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+print(f"op-only on a side stream: host issue {(t1 - t0) * 1e6 / calls:.1f} us/call, wall "
+      f"{(t2 - t0) * 1e6 / calls:.1f}, device (events) {e0.elapsed_time(e1) * 1e3 / calls:.1f}", flush=True)
