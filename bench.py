@@ -242,6 +242,34 @@ def bench_config(cfg, dev, rank, world, barrier_sync, max_over_ranks, steps):
               "step_mfma_frac_excl_a1": round((sum(fwd_f) + sum(bwd_f) - a1_fl) /
                                               (((st_us - (0 if resident else g_us))) * 1e-6) /
                                               FP32_MFMA_PEAK, 4)}
+    # configs 3 / 5 name 8 chains (on 8 GPUs in the reference): here 8 chains per GPU in one launch
+    # sequence of the multi-chain engine (its own slice widths), started from this
+    # chain's state; aggregate chain-steps/s, reported beside the one-chain rate
+    chains8 = None
+    if cfg in (3, 5):
+        from dgprf import engine as E
+        eng = m._engine
+        me = E.Engine(eng.spec, 8, seed=rank_seed(40 + cfg, rank))
+        me.z.copy_(eng.z)
+        me.hyp.copy_(eng.hyp)
+        me.theta.copy_(eng.theta.expand(8, -1))
+        me.init_moments()
+        me.lik_log_var_source = eng.lik_log_var_source
+        me.build_omega()
+        gph = me.graph(X, Y, c["batch"], n, c["lr"], c["beta"], c["T"], 50)
+        gph.launch()
+        reps = 4
+        barrier_sync()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            gph.launch()
+        barrier_sync()
+        t8 = max_over_ranks(time.perf_counter() - t0)
+        assert torch.isfinite(me.theta).all(), f"config {cfg} 8-chain run diverged"
+        chains8 = {"chains_per_gpu": 8, "slices_per_layer": list(me.layout.ns[:L]),
+                   "chain_steps_per_s": round(world * 8 * reps * 50 / t8, 1),
+                   "us_per_step_all_chains": round(t8 * 1e6 / (reps * 50), 2)}
+        del gph, me
     # S posterior samples (the chain's W at S successive steps) scored by ONE add_samples call:
     # every sample in one launch of the predictive kernel (grid.z = sample), then the fold
     S = 3 if cfg == 5 else 10
@@ -293,7 +321,8 @@ def bench_config(cfg, dev, rank, world, barrier_sync, max_over_ranks, steps):
            "predictive_flops_per_sample": int(fp),
            "predictive_a1": ("X_test Omega_1 resident, shared by every sample (not counted)"
                              if pred_a1_shared else None),
-           "a1_gemm": a1}
+           "a1_gemm": a1,
+           "chains8_per_gpu": chains8}
     del m, acc, X, Y, Xt, Yt
     torch.cuda.empty_cache()
     return out
