@@ -39,9 +39,11 @@ StepDev make_step_dev(const dgprf_plan_t& pl, const dgprf_chain_t& ch, const dgp
   sd.bd.y_cols = b.y_cols;
   sd.bd.mode = b.mode;
   // resident A_1 rows (wide first layer, fixed Omega_1, a dataset to gather from); enqueue_step
-  // drops it for full-Bayes steps (Omega_1 changes in-step)
+  // drops it for full-Bayes steps (Omega_1 changes in-step).  Per-chain hyper-parameters with
+  // several chains give every chain its own Omega_1, which one [n][R_1] projection cannot serve:
+  // ignored there (the GEMM runs per chain)
   const bool res = b.A1 && pl.a0_off >= 0 && b.mode != DGPRF_BATCH_DIRECT && !(pl.fresh_z & 1) &&
-                   pl.n_rf[0] % 4 == 0;
+                   pl.n_rf[0] % 4 == 0 && !(pl.hyp_per_chain && pl.n_chains > 1);
   sd.bd.A1 = res ? b.A1 : nullptr;
   sd.bd.a1_ld = pl.n_rf[0];
   sd.bd.pad = 0;
@@ -523,6 +525,8 @@ int dgprf_forward_samples(const dgprf_plan_t* plan, const float* thetas, int32_t
   if (plan->likelihood == DGPRF_LIK_GAUSSIAN && y_cols < plan->n_gp[plan->n_layers - 1])
     return DGPRF_E_SHAPE;
   if (scratch_floats < 0 || (scratch_floats > 0 && !scratch)) return DGPRF_E_ARG;
+  // one resident projection serves one Omega_1: not per-chain hyper-parameters over several chains
+  if (A1 && plan->hyp_per_chain && plan->n_chains > 1) return DGPRF_E_ARG;
   if (!A1 && scratch_floats < dgprf::forward_cfg(*plan, n).scratch_floats) return DGPRF_E_ARG;
   return hip_rc(dgprf::launch_forward_samples(*plan, thetas, n_samples, omega, der, X, A1, Y, y_cols,
                                               n, lse_m, lse_s, se_sum, scratch, scratch_floats,

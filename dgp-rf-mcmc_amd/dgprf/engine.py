@@ -12,6 +12,7 @@ stream; torch only provides memory, streams and collectives.
 """
 import ctypes
 import math
+import weakref
 
 import numpy as np
 import torch
@@ -189,9 +190,29 @@ class ModelSpec:
                            hyp_per_chain, self.ard)
 
 
+class _A1Entry:
+    """One resident first-layer projection: the dataset tensor it was computed from (weakly held,
+    so the entry cannot outlive it or be matched by another tensor at the same address), its buffer
+    and the Omega_1 state it reflects."""
+    __slots__ = ("xref", "buf", "okey", "__weakref__")
+
+    def __init__(self, X, buf, okey):
+        self.xref = weakref.ref(X)
+        self.buf = buf
+        self.okey = okey
+
+
+def _a1_drop(eng_ref, key, ent_ref):
+    """weakref.finalize callback of a dataset tensor: forget its projection (if still cached)."""
+    eng, ent = eng_ref(), ent_ref()
+    if eng is not None and ent is not None and eng._a1_cache.get(key) is ent:
+        del eng._a1_cache[key]
+
+
 class Engine:
     MAX_GRAPHS = 8  # instantiated step graphs kept per engine (LRU)
     A1_MAX_BYTES = 8 << 30  # resident first-layer projections (dataset_a1) larger than this: GEMM
+    A1_MAX_ENTRIES = 4  # resident projections kept per engine (LRU; graphs keep their own alive)
 
     def __init__(self, spec, n_chains=1, dev=None, seed=None, per_chain_hyp=None):
         """per_chain_hyp: every chain owns its kernel / likelihood hyper-parameters (and Omega),
@@ -338,8 +359,18 @@ class Engine:
             t.copy_(a.to(t.device))
         self.seed = int(np.asarray(st["seed"], dtype=np.uint64)[0])
         self.moments_ready, self.hyper_moments_ready = bool(mr), bool(hmr)
+        # captured graphs hold the old Philox key (chain_struct.seed at capture) and resident
+        # projections the old Omega_1: neither may be replayed / read after a load
+        self.drop_graphs()
+        self._a1_cache.clear()
         self.invalidate_omega()
         self.build_omega()
+
+    def drop_graphs(self):
+        """Destroy every cached step graph (after the stream drained: replays are asynchronous)."""
+        if self._graphs:
+            torch.cuda.current_stream(self.dev).synchronize()
+            self._graphs.clear()
 
     # ---------------------------------------------------------------- per-B plans
     def plan_ws(self, B, fresh_z=0, full_bayes=False):
@@ -454,7 +485,11 @@ class Engine:
         `tf.matmul(x, self.Omega)` (layers/rf_layers.py:42) for a wide first layer (d_1 > 32),
         computed once by the hand-written MFMA GEMM (dgprf_rf_project) instead of per minibatch /
         per posterior sample.  None when the layer is not wide, Omega_1 is per chain, or the
-        projection would exceed A1_MAX_BYTES.  Call after Omega is built."""
+        projection would exceed A1_MAX_BYTES.  Call after Omega is built.
+
+        An entry belongs to the X tensor object it was computed from (held by a weak reference and
+        dropped when X is freed), so another dataset later placed at the same address by the
+        caching allocator is projected afresh; at most A1_MAX_ENTRIES are kept (LRU)."""
         pl = self.layout
         if pl.a0_off < 0 or not self.resident_a1 or (self.per_chain_hyp and self.C > 1):
             return None
@@ -462,14 +497,22 @@ class Engine:
         rows = (n + 63) // 64 * 64
         if rows * R0 * 4 > self.A1_MAX_BYTES or R0 % 4:
             return None
-        key = (X.data_ptr(), tuple(X.shape))
+        key = (id(X), X.data_ptr(), tuple(X.shape))
         okey = (X._version, self._omega_key(), self.hyper_epoch)
-        ent = self._a1_cache.get(key)
-        if ent is None or ent[1] != okey:
-            buf = ent[0] if ent is not None else torch.zeros(rows, R0, dtype=_F32, device=self.dev)
+        ent = self._a1_cache.pop(key, None)
+        if ent is not None and ent.xref() is not X:
+            ent = None  # a dead tensor's entry (its finaliser has not run yet)
+        if ent is None or ent.okey != okey:
+            buf = ent.buf if ent is not None else torch.zeros(rows, R0, dtype=_F32, device=self.dev)
             self.rf_project(X, self.omega_view(0), out=buf[:n])
-            self._a1_cache[key] = (buf, okey)
-        return self._a1_cache[key][0]
+            if ent is None:
+                ent = _A1Entry(X, buf, okey)
+                weakref.finalize(X, _a1_drop, weakref.ref(self), key, weakref.ref(ent))
+            ent.okey = okey
+        self._a1_cache[key] = ent  # most recently used last
+        while len(self._a1_cache) > self.A1_MAX_ENTRIES:
+            self._a1_cache.pop(next(iter(self._a1_cache)))
+        return ent.buf
 
     # ---------------------------------------------------------------- hot path
     def _prep_batch(self, X, Y, stage=False):
@@ -583,10 +626,12 @@ class Engine:
         # resident X Omega_1 (graphs hold its pointer; refreshed in place here when stale, so a
         # cached graph's rows follow the current Omega_1)
         a1 = None if (full_bayes or (fresh_z & 1)) else self.dataset_a1(X_all)
+        # a graph holds the resident projection's buffer and the Philox key it was captured with
         key = (X_all.data_ptr(), tuple(X_all.shape), Y_all.data_ptr(), tuple(Y_all.shape),
                int(batch_size), float(data_size), float(lr), float(beta), float(T),
                int(steps_per_graph), int(schedule), int(start_step), int(cycle_length),
-               bool(resample_head), int(perm_seed), bool(full_bayes), int(fresh_z), a1 is not None)
+               bool(resample_head), int(perm_seed), bool(full_bayes), int(fresh_z),
+               0 if a1 is None else a1.data_ptr(), int(self.seed))
         if key in self._graphs:
             g = self._graphs.pop(key)  # most recently used last
             self._graphs[key] = g
@@ -608,7 +653,8 @@ class Engine:
         h = ctypes.c_void_p()
         N.call("dgprf_graph_create_sghmc", ctypes.byref(h), ctypes.byref(pl), ctypes.byref(ch),
                ctypes.byref(bt), ctypes.byref(st), int(steps_per_graph))
-        g = _Graph(h, (X_all, Y_all, ws, a1), int(steps_per_graph))
+        g = _Graph(h, (X_all, Y_all, ws, a1), int(steps_per_graph),
+                   weakref.ref(self) if full_bayes else None)
         self._graphs[key] = g
         return g
 
@@ -782,12 +828,20 @@ class Engine:
 
 
 class _Graph:
-    def __init__(self, handle, keep, steps=0):
+    def __init__(self, handle, keep, steps=0, hyper_engine=None):
         self.h = handle
         self._keep = keep
         self.steps = steps  # SGHMC steps one replay runs
+        # full_bayesian=True graphs: every replay rewrites hyp / Omega on the device, which torch's
+        # version counters do not see — each launch advances the engine's hyper_epoch, so a
+        # resident projection (dataset_a1) made from the old Omega_1 is recomputed
+        self._hyper_engine = hyper_engine
 
     def launch(self):
+        if self._hyper_engine is not None:
+            eng = self._hyper_engine()
+            if eng is not None:
+                eng.hyper_epoch += 1
         N.call("dgprf_graph_launch", self.h, stream())
 
     def __del__(self):

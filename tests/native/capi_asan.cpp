@@ -237,6 +237,14 @@ int main() {
                               nullptr, 0, nullptr) == DGPRF_E_ARG);
   CHECK(dgprf_forward_samples(&ok, &f, 2, &f, &f, &f, nullptr, &f, 1, 10, &f, &f, nullptr,
                               nullptr, -1, nullptr) == DGPRF_E_ARG);
+  {  // a resident A_1 with per-chain hyper-parameters over several chains (one Omega_1 each)
+    const int kw[1] = {DGPRF_RBF}, rw[1] = {64}, gw[1] = {1};
+    dgprf_plan_t pc = make(1, 40, 1, kw, rw, gw, 10, 2);
+    pc.hyp_per_chain = 1;
+    CHECK(dgprf_plan_init(&pc) == DGPRF_OK && pc.a0_off >= 0);
+    CHECK(dgprf_forward_samples(&pc, &f, 2, &f, &f, &f, &f, &f, 1, 10, &f, &f, nullptr,
+                                nullptr, 0, nullptr) == DGPRF_E_ARG);
+  }
   CHECK(dgprf_lse_finalize(&f, &f, nullptr, 0, 10, 1.0, 0.f, 1.f, nullptr, nullptr, nullptr) ==
         DGPRF_E_ARG);
   CHECK(dgprf_rf_omega(9, 1, 1, &f, &f, &f, &f, &f, &f, nullptr) == DGPRF_E_ARG);

@@ -44,7 +44,15 @@ def _worker(rank, world, port, q):
     m = torch.tensor(np.stack(ms))
     s = torch.tensor(np.stack(ss))
     e = torch.tensor(se.sum(axis=1))
+    calls = []  # every collective gather_accumulators issues
+    for name in ("all_gather", "all_reduce", "all_gather_into_tensor", "broadcast"):
+        f = getattr(dist, name)
+        setattr(dist, name, (lambda f, name: lambda *a, **k: (calls.append(name), f(*a, **k))[1])(
+            f, name))
     M, Sa, E, S_tot = D.gather_accumulators(m, s, e, C * S)
+    assert calls == ["all_gather"], calls  # (m | s | e | S) packed into one exchange
+    M2, S2, E2, _ = D.gather_accumulators(m, s, None, C * S)  # a softmax model: no se sums
+    assert E2 is None and torch.equal(M2, M) and torch.equal(S2, Sa)
     assert M.shape == (world * C, n) and S_tot == world * C * S
     if rank == 0:
         q.put((M.numpy(), Sa.numpy(), E.numpy(), S_tot))

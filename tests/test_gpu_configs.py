@@ -396,7 +396,7 @@ def test_resident_first_layer_projection_steps(dev):
         with torch.no_grad():  # MCEM-style in-place update: Omega_1 and the projection rebuild
             for mm in models:
                 mm.kernel_list[0].log_inv_length_scale.sub_(0.1)
-    buf = next(iter(a._engine._a1_cache.values()))[0]
+    buf = next(iter(a._engine._a1_cache.values())).buf
     ref = X.double() @ a._engine.omega_view(0).double()
     assert float((buf[:n].double() - ref).abs().max()) <= 2e-5 * float(ref.abs().max())
     assert torch.all(buf[n:] == 0)
@@ -487,3 +487,176 @@ def test_config4_predictive_rows_agemm_128(dev):
     lp = cpu(m._engine.forward(Xt, Yt, logp=True)["logp"][0])
     ref = O.log_prob(p, O.forward(p, Xt), Yt)
     assert np.max(np.abs(lp - ref)) < 2e-5 * max(1.0, np.max(np.abs(ref)))
+
+
+# ------------------------------------------------------------------ config 4's benchmarked step
+# path: the resident X Omega_1 of the whole training set (Engine.dataset_a1) gathered per step in
+# ceil(4096 / 1024) = 4 parts per row (gather_a1_part), read by the 8-wave layer-0 kernels
+def _config4_resident_grad(eng, Xd, Yd, idx, N_, a1):
+    """dU/dW [C, w_total] of the INDEXED minibatch idx [C, B] through the C-ABI dgprf_potential_grad
+    (k_gather's resident-A_1 blocks for the rows, then the step's forward / backward) — with the
+    dataset's resident projection a1, or the per-step A_1 GEMM when a1 is None."""
+    import ctypes
+    from dgprf import _native as N
+    from dgprf.engine import ptr, stream
+    B = idx.shape[1]
+    pl, ws = eng.plan_ws(B)
+    G = torch.zeros(eng.C, pl.w_total, device=Xd.device)
+    ch = eng.chain_struct(ws)
+    it = torch.as_tensor(idx, dtype=torch.int32, device=Xd.device).contiguous()
+    bt = eng.batch_struct(Xd, Yd, N.BATCH_INDEXED, idx=it)
+    bt.A1 = None if a1 is None else a1.data_ptr()
+    N.call("dgprf_potential_grad", ctypes.byref(pl), ctypes.byref(ch), ctypes.byref(bt),
+           float(N_), 0, ptr(G), stream())
+    torch.cuda.synchronize()
+    return G
+
+
+def _config4_data(dev, n, seed):
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    X = torch.rand(n, 784, device=dev, generator=g) - 0.5  # normalize_MNIST range
+    Y = torch.randint(0, 10, (n, 1), device=dev, generator=g).float()
+    return X, Y
+
+
+@pytest.mark.parametrize("C", [1, 4])
+def test_config4_resident_a1_grad_vs_oracle(dev, C):
+    """Config 4's full model (784 -> 4 x RBF n_rf 4096, g [30,30,30,10], softmax) at its benchmarked
+    B = 200 over N = 60,000 rows: the gradient of an INDEXED minibatch whose first-layer rows are
+    gathered from the resident X Omega_1 (4 gather parts of 1,024 features per row) against the
+    float64 oracle (layers/rf_layers.py:42; models/dgp.py:194-198) for chain 0 and the last chain,
+    and against the same step with the per-step A_1 GEMM; C = 4 chains sharing one hyper-parameter
+    set (dataset_a1 serves them all) with their own rows and W."""
+    import copy
+    from dgprf import engine as E
+    c = CONFIGS[4]
+    m, p = _model(c, 70 + C)
+    one = m._engine
+    eng = one if C == 1 else E.Engine(one.spec, C, seed=one.seed)
+    if C > 1:
+        assert not eng.per_chain_hyp
+        eng.z.copy_(one.z)
+        eng.hyp.copy_(one.hyp)
+        scale = 1.0 + 0.05 * torch.arange(C, device=dev, dtype=torch.float32)[:, None]
+        eng.theta.copy_(one.theta[:1] * scale)
+    eng.build_omega()
+    n, B, N_ = 60_000, 200, 60_000
+    Xd, Yd = _config4_data(dev, n, 404)
+    a1 = eng.dataset_a1(Xd)
+    assert a1 is not None and eng.layout.a0_off >= 0 and (eng.layout.n_rf[0] + 1023) // 1024 == 4
+    rng = np.random.default_rng(405 + C)
+    idx = np.stack([rng.choice(n, B, replace=False) for _ in range(C)]).astype(np.int32)
+    G = _config4_resident_grad(eng, Xd, Yd, idx, N_, a1)
+    Gg = _config4_resident_grad(eng, Xd, Yd, idx, N_, None)  # the per-step GEMM form
+    assert torch.isfinite(G).all() and float(G.abs().max()) > 0
+    for chain in range(C):
+        for l, (x, y) in enumerate(zip(unpack(eng, G, chain), unpack(eng, Gg, chain))):
+            assert rel_err(x, y) < 2e-5, ("resident vs GEMM", chain, l)
+    Xh, Yh = cpu(Xd), cpu(Yd)
+    for chain in sorted({0, C - 1}):
+        pc = copy.copy(p)
+        s = np.float64(np.float32(1.0 + 0.05 * chain))
+        pc.W = [w * s for w in p.W]
+        ref = O.grad_W(pc, Xh[idx[chain]], Yh[idx[chain]], N_)
+        got = unpack(eng, G, chain=chain)
+        for l in range(4):
+            assert rel_err(got[l], ref[l]) < 2e-4, (C, chain, l)
+
+
+def test_config4_resident_a1_graph_steps(dev):
+    """Config 4's benchmarked step path as the bench runs it: W-only graph replays (2 x 5 steps, the
+    first step of each replay gathering its A_1 rows in k_gather, the next ones in the update
+    kernel's gather blocks) at B = 200 over N = 60,000 rows with the resident projection, against
+    the same 10 steps with the per-step A_1 GEMM from the same state: theta within 2e-5 of its
+    scale, and a third model replaying the resident path bit-identically."""
+    from dgprf import engine as E
+    c = CONFIGS[4]
+    models = []
+    for _ in range(3):
+        m, _ = _model(c, 77)
+        models.append(m)
+    a, b, r = models
+    b._engine.resident_a1 = False
+    n = 60_000
+    X, Y = _config4_data(dev, n, 406)
+    for mm in models:
+        E.set_seed(78)
+        mm.precond_update(None, n, precond_type="identity")
+    for mm in (b, r):
+        mm._engine.mom.copy_(a._engine.mom)
+        mm._engine.theta.copy_(a._engine.theta)
+    run = dict(batch_size=200, lr=0.01, momentum_decay=0.9, steps_per_graph=5, perm_seed=9)
+    for mm in models:
+        mm.run_sgmcmc(X, Y, n, 10, **run)
+    torch.cuda.synchronize()
+    assert a._engine._a1_cache and not b._engine._a1_cache
+    ta, tb = a._engine.theta, b._engine.theta
+    assert torch.isfinite(ta).all()
+    assert float((ta - tb).abs().max()) <= 2e-5 * float(tb.abs().max())
+    assert torch.equal(ta, r._engine.theta)
+
+
+# ------------------------------------------------------------------ resident projection cache
+def test_dataset_a1_same_address_new_dataset(dev):
+    """Two same-shape test sets created one after the other (the caching allocator hands the second
+    the first one's block): each is scored against its own projection — equal to the GEMM path —
+    and a freed dataset's entry leaves the cache."""
+    import gc
+    from dgprf import engine as E
+    from dgprf.predictive import PredictiveLSE
+    from likelihoods import Softmax
+    from models.dgp import DGP_RF
+    E.set_seed(81)
+    m = DGP_RF(100, 5, n_hidden_layers=2, n_rf=[256, 128], n_gp=[10, 5], likelihood=Softmax(),
+               kernel_type_list=["RBF", "RBF"])
+    eng = m._engine
+    ptrs = []
+    for seed in (1, 2):
+        Xt = torch.rand(3000, 100, device=dev) * 2 - 1 + 0.1 * seed
+        Yt = torch.randint(0, 5, (3000, 1), device=dev).float()
+        ptrs.append(Xt.data_ptr())
+        acc = PredictiveLSE(eng, Xt, Yt)
+        acc.add_sample()
+        ll, _ = acc.finalize()
+        eng.resident_a1 = False
+        ref = PredictiveLSE(eng, Xt, Yt)
+        ref.add_sample()
+        ll_ref, _ = ref.finalize()
+        eng.resident_a1 = True
+        assert abs(ll - ll_ref) < 1e-5 * max(1.0, abs(ll_ref)), seed
+        assert len(eng._a1_cache) == 1
+        del acc, ref, Xt, Yt
+        gc.collect()
+        assert not eng._a1_cache  # the finaliser dropped the freed dataset's projection
+    assert ptrs[0] == ptrs[1], "allocator did not reuse the block: the case is not exercised"
+
+
+def test_full_bayes_graph_replay_invalidates_projection(dev):
+    """Full-Bayes graphs taken from sgmcmc_graphs and launched directly rewrite hyp / Omega_1 on the
+    device at every replay: each launch advances hyper_epoch, so dataset_a1 afterwards is the
+    projection of the CURRENT Omega_1, not of the one before the replays."""
+    from dgprf import engine as E
+    from likelihoods import Softmax
+    from models.dgp import DGP_RF
+    E.set_seed(82)
+    m = DGP_RF(100, 5, n_hidden_layers=2, n_rf=[256, 128], n_gp=[10, 5], likelihood=Softmax(),
+               kernel_type_list=["RBF", "RBF"])
+    eng = m._engine
+    n = 2000
+    X = torch.rand(n, 100, device=dev) * 2 - 1
+    Y = torch.randint(0, 5, (n, 1), device=dev).float()
+    m.precond_update(None, n, precond_type="identity", full_bayesian=True)
+    Xt = torch.rand(500, 100, device=dev) * 2 - 1
+    plan = m.sgmcmc_graphs(X, Y, n, 20, batch_size=100, lr=0.05, momentum_decay=0.9,
+                           steps_per_graph=10, full_bayesian=True)
+    before = eng.dataset_a1(Xt).clone()
+    ep = eng.hyper_epoch
+    for g, reps in plan:
+        for _ in range(reps):
+            g.launch()
+    assert eng.hyper_epoch == ep + 2
+    now = eng.dataset_a1(Xt)
+    ref = Xt.double() @ eng.omega_view(0).double()
+    assert float((now[:500].double() - ref).abs().max()) <= 2e-5 * float(ref.abs().max())
+    assert not torch.equal(now[:500], before[:500])  # Omega_1 did move

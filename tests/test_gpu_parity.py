@@ -404,9 +404,10 @@ def test_per_call_host_batches_equal_device_batches(dev):
 
 
 def test_checkpoint_resume_bit_exact(dev, tmp_path):
-    """save() at step 100 -> load() into a freshly built model -> 100 more graph-replayed steps is
-    bitwise the 200 uninterrupted steps (SURVEY §5 checkpoint / resume; the reference keeps only
-    live variable aliases, experiments/utils_training.py:226)."""
+    """save() at step 100 -> load() into another model (one that has already captured and replayed
+    its own step graphs) -> 100 more graph-replayed steps is bitwise the 200 uninterrupted steps
+    (SURVEY §5 checkpoint / resume; the reference keeps only live variable aliases,
+    experiments/utils_training.py:226)."""
     from likelihoods import Gaussian
     from models.regression_model import RegressionDGP
     from dgprf import engine as E
@@ -425,6 +426,11 @@ def test_checkpoint_resume_bit_exact(dev, tmp_path):
     a.run_sgmcmc(X, Y, n, 100, **run)
     E.set_seed(999)  # a different construction draw: everything must come from the checkpoint
     b = mk()
+    # b has already captured (and replayed) graphs of the same arguments under its own Philox key:
+    # load() must not leave them to be replayed with the old key
+    b.precond_update(None, n, precond_type="identity")
+    b.run_sgmcmc(X, Y, n, 100, **run)
+    assert b._engine._graphs
     b.load(path)
     assert int(b._engine.step_ctr) == 100 and b._engine.seed == a._engine.seed
     assert b.W_mcmc[0].moments is not None
