@@ -514,6 +514,13 @@ class Engine:
             self._a1_cache.pop(next(iter(self._a1_cache)))
         return ent.buf
 
+    def invalidate_a1(self):
+        """Mark every resident projection stale: the next dataset_a1 recomputes it into the same
+        buffer (so graphs holding that buffer stay valid) — e.g. to time the projection inside a
+        measured region."""
+        for ent in self._a1_cache.values():
+            ent.okey = None
+
     # ---------------------------------------------------------------- hot path
     def _prep_batch(self, X, Y, stage=False):
         """stage: X, Y are one call's batch (never a dataset a graph keeps): host arrays go through

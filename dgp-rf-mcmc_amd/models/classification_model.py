@@ -2,7 +2,7 @@
 import torch
 
 from likelihoods import Softmax
-from models.dgp import DGP_RF
+from models.dgp import DGP_RF, whole_dataset
 
 
 class ClassificationDGP(DGP_RF):
@@ -43,6 +43,9 @@ class ClassificationDGP(DGP_RF):
     def eval_log_likelihood(self, ds):
         """log p(Y|F) per test point [N] (:49-60), fused forward + softmax likelihood kernel."""
         om = self._omega_for_call()
+        whole = whole_dataset(ds)
+        if whole is not None:  # every row in one fused launch (same rows, same order)
+            return self._engine.forward(*whole, logp=True, omega=om, build=False)["logp"][0]
         log_p_all_data = []
         for x_batch, y_batch in ds:
             out = self._engine.forward(x_batch, y_batch, logp=True, omega=om, build=False)

@@ -18,6 +18,22 @@ from likelihoods import Gaussian, Softmax
 from utils import BNN_from_list, BNN_from_list_input_cat, log_gaussian
 
 
+def whole_dataset(ds):
+    """(X, Y) of an in-order, single-pass DeviceDataset (experiments/utils_dataset.py), else None.
+    Rows of the DGP forward are independent, so scoring such a dataset batch by batch
+    (models/regression_model.py:33-50, classification_model.py:49-60) and concatenating equals ONE
+    forward over all its rows: one launch instead of one per batch (1e5 test rows at the driver's
+    B = 200: 500 launches)."""
+    from experiments.utils_dataset import DeviceDataset
+    if isinstance(ds, DeviceDataset) and not ds.shuffled and not ds.repeated:
+        B = ds.batch_size
+        if not ds.drop_remainder or not B:
+            return ds.X, ds.Y
+        n = ds.n // B * B  # the batches drop the remainder rows
+        return ds.X[:n], ds.Y[:n]
+    return None
+
+
 def _per_layer(v, L, what):
     """Scalar -> [v]*L, list -> list (models/dgp.py:34-43)."""
     if np.ndim(v) == 0:

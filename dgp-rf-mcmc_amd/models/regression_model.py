@@ -2,7 +2,7 @@
 import torch
 
 from likelihoods import Gaussian
-from models.dgp import DGP_RF
+from models.dgp import DGP_RF, whole_dataset
 
 
 class RegressionDGP(DGP_RF):
@@ -38,10 +38,15 @@ class RegressionDGP(DGP_RF):
         """
         :param ds: iterable X: [N, D_in]; Y: [N, D_out];
         :return: log likelihood log p(Y|F) [N] and square errors [N] (:33-50), one fused
-                 forward + likelihood kernel per batch.
+                 forward + likelihood kernel per batch (one over the whole set for an in-order
+                 DeviceDataset).
         """
         assert isinstance(self.likelihood, Gaussian), "The likelihood of the model is not Gaussian!"
         om = self._omega_for_call()
+        whole = whole_dataset(ds)
+        if whole is not None:  # every row in one fused launch (same rows, same order)
+            out = self._engine.forward(*whole, logp=True, se=True, omega=om, build=False)
+            return out["logp"][0], out["se"][0]
         log_p_all_data, se_all_data = [], []
         for x_batch, y_batch in ds:
             out = self._engine.forward(x_batch, y_batch, logp=True, se=True, omega=om, build=False)

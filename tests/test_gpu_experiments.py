@@ -154,3 +154,37 @@ def test_mcem_end_to_end(dev):
     assert tuple(log_p.shape) == (3, 97) and torch.isfinite(log_p).all()
     dh = (m._engine.hyp - h0).abs()
     assert float(dh.max()) > 0.01  # Adam moved the kernel / likelihood hyper-parameters
+
+
+def test_eval_whole_test_set_equals_batches(dev):
+    """eval_log_likelihood_and_se / eval_log_likelihood over an in-order DeviceDataset score every
+    row in ONE forward (models.dgp.whole_dataset) instead of one per batch: the same rows in the
+    same order as the batch loop (a plain list of the same batches, whose per-batch forward the
+    parity tests pin to the oracle), to fp32 rounding of another kernel path; a drop_remainder set
+    leaves out the same rows."""
+    from dgprf import engine as E
+    from experiments.utils_dataset import DeviceDataset, load_arrays
+    from likelihoods import Gaussian, Softmax
+    from models.classification_model import ClassificationDGP
+    from models.regression_model import RegressionDGP
+    X, Y, Xs, Ys = _small_regression(2, n_test=1003)
+    E.set_seed(11)
+    m = RegressionDGP(3, 1, n_hidden_layers=2, n_rf=[64, 32], n_gp=[3, 1],
+                      likelihood=Gaussian(variance=0.1))
+    _, ds_test, _, _ = load_arrays(X, Y, Xs, Ys, batch_size=100)
+    lp, se = m.eval_log_likelihood_and_se(ds_test)
+    lp_b, se_b = m.eval_log_likelihood_and_se([(x, y) for x, y in ds_test])
+    assert lp.shape == (1003,) and se.shape == (1003,)
+    scale = float(lp_b.abs().max())
+    assert float((lp - lp_b).abs().max()) <= 2e-6 * scale
+    assert float((se - se_b).abs().max()) <= 2e-6 * float(se_b.abs().max())
+    dr = DeviceDataset(Xs, Ys).batch(100, drop_remainder=True)
+    assert m.eval_log_likelihood_and_se(dr)[0].shape == (1000,)
+    E.set_seed(12)
+    c = ClassificationDGP(3, 4, n_hidden_layers=2, n_rf=[64, 32], n_gp=[5, 4],
+                          likelihood=Softmax())
+    Yc = (np.abs(Ys * 7).astype(np.int64) % 4).astype(np.float32)
+    ds_c = DeviceDataset(Xs, Yc).batch(128)
+    lc = c.eval_log_likelihood(ds_c)
+    lc_b = c.eval_log_likelihood([(x, y) for x, y in ds_c])
+    assert float((lc - lc_b).abs().max()) <= 2e-6 * float(lc_b.abs().max())
