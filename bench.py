@@ -714,17 +714,22 @@ def main():
     att = [max(x - prof["empty"], 1e-6) for x in inflow]
     Lk = len(prof["fwd"])
     att_fwd, att_bwd, att_upd = att[:Lk], att[Lk:2 * Lk], att[2 * Lk]
+    # a folded output layer (plan.fold_out) launches no forward: its F_L is formed inside its
+    # backward, whose launch then carries that layer's forward FLOPs as well
+    fold = int(eng.plan_ws(B)[0].fold_out)
+    n_fwd = Lk - fold
     per_name = {
-        "k_step_fwd": (sum(att_fwd) / Lk, sum(fwd_f) / Lk, Lk),
-        "k_step_bwd": (sum(att_bwd) / Lk, sum(bwd_f) / Lk, Lk),
+        "k_step_fwd": (sum(att_fwd[:n_fwd]) / n_fwd, sum(fwd_f[:n_fwd]) / n_fwd, n_fwd),
+        "k_step_bwd": (sum(att_bwd) / Lk, (sum(bwd_f) + (fwd_f[-1] if fold else 0)) / Lk, Lk),
     }
     upd_bytes = 4 * pl.w_total * (pl.n_row_tiles + 2 + 2 + 2)  # gW partials + theta/mom r/w
     dom = max(per_name, key=lambda k: per_name[k][0] * per_name[k][2])
     ms_dom, fl_dom, _ = per_name[dom]
     rp_us = rocprof_avg_us(dom)
     n_dom = per_name[dom][2]
-    dom_pairs = inflow[:Lk] if dom == "k_step_fwd" else inflow[Lk:2 * Lk]
-    share_us = step_ms_dev * 1e3 * sum(dom_pairs) / sum(inflow) / n_dom
+    launched = inflow[:n_fwd] + inflow[Lk:]  # the event pairs around launched kernels
+    dom_pairs = inflow[:n_fwd] if dom == "k_step_fwd" else inflow[Lk:2 * Lk]
+    share_us = step_ms_dev * 1e3 * sum(dom_pairs) / sum(launched) / n_dom
     live_us = ms_dom * 1e3
     # duration per launch (`achieved` / `frac`): the committed rocprofv3 kernel trace of this bench
     # (profiles/rNN/kernel_stats_bench.csv, dispatch-weighted mean over the kernel's instances), so
@@ -737,7 +742,7 @@ def main():
     if rp_us and os.path.exists(tr_path):
         with open(tr_path) as fh:
             trace_step_us = json.load(fh)["roofline"]["step_us_events"]
-    n_launch = 2 * len(d) + 1
+    n_launch = 2 * len(d) + 1 - fold
     bnd_us = launch_boundary_us(dev)
     rel = os.path.relpath(PROFILES, ROOT)
     roof = {"kernel": dom, "bound": "mfma",
@@ -781,7 +786,8 @@ def main():
             "rocprof_scaled_us": (round(rp_us * step_ms_dev * 1e3 / trace_step_us, 3)
                                   if rp_us and trace_step_us else None),
             "empty_pair_us": round(prof["empty"] * 1e3, 3),
-            "step_kernel_us": {"fwd": [round(x * 1e3, 3) for x in att_fwd],
+            "output_layer_folded": bool(fold),
+            "step_kernel_us": {"fwd": [round(x * 1e3, 3) for x in att_fwd[:n_fwd]],
                                "bwd": [round(x * 1e3, 3) for x in att_bwd],
                                "update": round(att_upd * 1e3, 3)},
             "inflow_event_us": [round(x * 1e3, 3) for x in inflow],

@@ -131,7 +131,9 @@ hipError_t enqueue_step(const dgprf_plan_t& pl, const StepDev& sd_in, const Upda
   if (dgprf_sk::step_fused_fwd(pl)) {  // large B, one chain: one all-layer forward launch
     if (e == hipSuccess) e = dgprf::launch_step_fwd_fused(pl, sd, s);
   } else {
-    for (int l = 0; l < pl.n_layers && e == hipSuccess; ++l) e = dgprf::launch_step_fwd(pl, sd, l, s);
+    // a folded output layer (plan.fold_out, W-only) is formed inside its backward: no launch
+    const int nf = pl.fold_out && !sd.full_bayes ? pl.n_layers - 1 : pl.n_layers;
+    for (int l = 0; l < nf && e == hipSuccess; ++l) e = dgprf::launch_step_fwd(pl, sd, l, s);
   }
   for (int l = pl.n_layers - 1; l >= 0 && e == hipSuccess; --l)
     e = dgprf::launch_step_bwd(pl, sd, l, s);
@@ -259,7 +261,7 @@ int dgprf_plan_init(dgprf_plan_t* pl) {
   // keeps its gW in accumulators (k_step_bwd_rg), so the gW partials stay <= 16 rows
   pl->rt_per_group = 1;
   pl->rg_full_bayes = 0;
-  pl->pad1 = 0;
+  pl->fold_out = 0;
   if (pl->n_row_tiles > 16 && !pl->bwd_tiles) {
     bool ok = true, ok_fb = true;
     dgprf_sk::RgCfg c;
@@ -312,6 +314,7 @@ int dgprf_plan_init(dgprf_plan_t* pl) {
   if (pl->rt_per_group > 1 && ws >= ((int64_t)1 << 29)) return DGPRF_E_SHAPE;
   pl->ws_chain = ws;
   pl->ws_total = ws * pl->n_chains;
+  pl->fold_out = dgprf_sk::step_fold_out(*pl) ? 1 : 0;
   pl->initialised = 1;
   return DGPRF_OK;
 }
@@ -465,6 +468,8 @@ int dgprf_profile_step(const dgprf_plan_t* plan, const dgprf_chain_t* chain,
       if (e != hipSuccess) break;
       if (kk < L && dgprf_sk::step_fused_fwd(*plan))  // one all-layer forward (timed as layer 0)
         e = kk == 0 ? dgprf::launch_step_fwd_fused(*plan, sd, s) : hipSuccess;
+      else if (kk == L - 1 && plan->fold_out)  // folded into the backward: an empty pair
+        e = hipSuccess;
       else if (kk < L) e = dgprf::launch_step_fwd(*plan, sd, kk, s, /*with_agemm=*/!ag);
       else if (kk < 2 * L) e = dgprf::launch_step_bwd(*plan, sd, kk - L, s);
       else e = dgprf::launch_step_update(*plan, sd, ud, nullptr, s);

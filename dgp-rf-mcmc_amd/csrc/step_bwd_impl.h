@@ -34,11 +34,70 @@ __device__ __forceinline__ void stage_slice_lds(const LayerK& a, const float* W,
 }
 
 
+// Folded output layer (a.rcf, RCF instances; step_fold_out): the layer's whole W_L [P] and Omega_L
+// rows [d][R + 16] copied global -> LDS with global_load_lds at kernel start (no VGPRs; in flight
+// with the prologue's partial-sum loads, waited for by its barrier).  W_L and Omega_L rows start
+// 16-byte aligned (w_off / omega_off multiples of 4) and R % 256 == 0.
+template <bool RBF>
+__device__ __forceinline__ void rcf_stage(const LayerK& a, const float* W, const float* om,
+                                          float* smem) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = (int)(blockDim.x >> 6);
+  const int R = a.R, P = RBF ? 2 * R : R, per_row = R >> 8;
+  float* wl = smem + a.rcf_off;
+  float* ol = wl + P;
+  for (int j = wave; j < (P >> 8); j += nw)
+    __builtin_amdgcn_global_load_lds(W + j * 256 + 4 * lane, wl + j * 256, 16, 0, 0);
+  for (int j = wave; j < a.d * per_row; j += nw) {
+    const int k = j / per_row, c = j - k * per_row;
+    __builtin_amdgcn_global_load_lds(om + (int64_t)k * R + c * 256 + 4 * lane,
+                                     ol + k * (R + 16) + c * 256, 16, 0, 0);
+  }
+}
+
+// This wave's share of F_L[row lr] = sum_f Phi[lr][f] W_L[f] (layers/rf_layers.py:42-44,
+// layers/GP_weight_layers.py:11-15, g_L = 1): 16-feature chunks wave, wave + 4, ... in order, the A
+// tile on v_mfma_f32_16x16x4_f32 from the staged Omega_L rows and the X tile, features and the W_L
+// dot product as in k_step_fwd's g = 1 body; summed over the lane's 4 features then the 4 feature
+// groups (every lane of row lr ends with the same value).
+template <int KS, bool RBF>
+__device__ __forceinline__ float rcf_row_partial(const LayerK& a, const float* smem,
+                                                 const float (&xf)[8], float cl, int wave, int lr,
+                                                 int lq) {
+  const int R = a.R, d = a.d, ost = R + 16, nch = R >> 4;
+  const float* wl = smem + a.rcf_off;
+  const float* ol = wl + (RBF ? 2 * R : R);
+  float acc = 0.f;
+  for (int c = wave; c < nch; c += 4) {
+    const int f0 = c * 16;
+    f4 at = f4zero();
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int k = 4 * ks + lq;
+      const float o = ol[(k < d ? k : d - 1) * ost + f0 + lr];  // rows >= d: not staged
+      at = mfma16(k < d ? o : 0.f, xf[ks], at);  // at[r] = A[row lr][f0 + 4 lq + r]
+    }
+    float p0[4], p1[4];
+    features<RBF>(at, cl, p0, p1);
+    const f4 w0 = *reinterpret_cast<const f4*>(wl + f0 + 4 * lq);
+    f4 w1 = f4zero();
+    if (RBF) w1 = *reinterpret_cast<const f4*>(wl + R + f0 + 4 * lq);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      acc = fmaf(p0[r], w0[r], acc);
+      if (RBF) acc = fmaf(p1[r], w1[r], acc);
+    }
+  }
+  acc += __shfl_xor(acc, 16);
+  acc += __shfl_xor(acc, 32);
+  return acc;
+}
+
 // NWB: waves per workgroup (8: W-only, whole-slice LDS image).  GSM: how the gW partial tile
 // leaves (1 < g): 0 = chosen at run time (g % 16 == 0: transposed tile, 16-byte lanes; else dword
 // stores from the MFMA tile), 1 = transposed tile only, 2 = staged per wave in LDS and stored as
 // contiguous 16-byte lanes only (a.gst_off).
-template <int KS, int NOT, bool RBF, bool G1, bool FB, int NWB, int GSM>
+// RCF: the folded output layer's instance (g = 1, W-only, 4 waves): F_L recomputed here.
+template <int KS, int NOT, bool RBF, bool G1, bool FB, int NWB, int GSM, bool RCF = false>
 __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT == 1 && !FB && (KS == 1 || KS == 2 || (KS == 4 && !RBF))) ? STEP_WPE : 1))) void k_step_bwd(const LayerK a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr bool WST = NWB == 8;  // whole-slice staging (a.wstage == 1 exactly then)
@@ -126,6 +185,7 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
   const float* yr = a.yrows + (int64_t)chain * a.yrow_cs;
   float* ysh = dfs + round4(TR * dfst);
   const int yc = a.likelihood == DGPRF_LIK_GAUSSIAN ? g : 1;
+  if (RCF) rcf_stage<RBF>(a, W, om, smem);  // the whole output layer, for the F_L recompute
   if (a.fast) {
     // ---- single burst: W/Omega block, X tile, dF (or F_L) partials and Y rows
     f4 sw[2], so;
@@ -162,6 +222,22 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
     }
   }
 
+  if (RCF) {
+    // folded output layer: F_L of this row tile from the X tile (F_{L-1}) and the staged layer,
+    // the 4 waves' feature shares summed in wave order into the dF tile (rows >= B: 0)
+    __syncthreads();  // X tile, Y values and the LDS copies of W_L / Omega_L
+    float xr[8];
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) xr[ks] = (ks < KS && 4 * ks < d) ? xs[lr * a.xst + 4 * ks + lq] : 0.f;
+    const float v = rcf_row_partial<KS, RBF>(a, smem, xr, cl, wave, lr, lq);
+    if (lq == 0) red[wave * TR + lr] = v;
+    __syncthreads();
+    if (threadIdx.x < TR) {
+      const int r = threadIdx.x;
+      const float f = ((red[r] + red[TR + r]) + red[2 * TR + r]) + red[3 * TR + r];
+      dfs[r * dfst] = row0 + r < B ? f : 0.f;
+    }
+  }
   // dF_l tile [16][g]: the last layer turns F_L into the likelihood gradient in place;
   // otherwise dF_l = dX_{l+1}[:, :g_l] (already summed above)
   if (a.last) {
@@ -541,6 +617,18 @@ void k_step_bwd_launch3(bool rbf, bool fb, bool w8, bool t16, dim3 grid, size_t 
     hipLaunchKernelGGL((k_step_bwd<KS, NOT, R_, G1, F_, W_, M_>), grid, dim3(64 * W_), lds, s, a); \
   } while (0)
   constexpr int GS = G1 ? 1 : 2;
+  if constexpr (G1 && KS > 0) {
+    if (a.rcf) {  // folded output layer (make_layer_k sets rcf only for 4-wave W-only launches)
+      if (rbf) {
+        dgprf::set_lds_limit((const void*)k_step_bwd<KS, NOT, true, G1, false, 4, 0, true>, lds);
+        hipLaunchKernelGGL((k_step_bwd<KS, NOT, true, G1, false, 4, 0, true>), grid, dim3(256), lds, s, a);
+      } else {
+        dgprf::set_lds_limit((const void*)k_step_bwd<KS, NOT, false, G1, false, 4, 0, true>, lds);
+        hipLaunchKernelGGL((k_step_bwd<KS, NOT, false, G1, false, 4, 0, true>), grid, dim3(256), lds, s, a);
+      }
+      return;
+    }
+  }
   if (rbf) {
     if (fb) DGPRF_BWD(true, true, 4, 0);
     else if (w8 && t16) DGPRF_BWD(true, false, 8, 1);

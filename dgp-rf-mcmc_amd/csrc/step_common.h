@@ -107,6 +107,8 @@ struct LayerK {
   int32_t rw_one;         // row-wave backward: the dF source is one complete slice (= last)
   int32_t cmp;           // row-group backward after the fused forward (step_fused_fwd): every
                          // F_l is complete in slice 0 of its partial buffer (one load, not 16)
+  int32_t rcf, rcf_off;  // output layer folded into its backward (step_fold_out): the layer's
+                         // whole W_L [P] and Omega_L [d][R + 16] staged in LDS at rcf_off
   unsigned long long* stamps;  // -DDGPRF_STAMPS diagnostic build: stamp buffer, else null
 };
 
@@ -284,7 +286,8 @@ __device__ __forceinline__ void elem_issue(const LayerK& a, int chain, int row0,
   const int c = isx ? u - r * dpad : ud - r * a.g;
   const int b = row0 + r;
   const bool inb = b < a.B && (isx || isd);
-  const bool fromp = inb && (isx ? c < a.gp : true);
+  // (a folded output layer forms its F_L tile itself: only its Y values are loaded here)
+  const bool fromp = inb && (isx ? c < a.gp : !a.rcf);
   const int w = isx ? a.gp : a.g;
   const int base = (isx ? a.fprev_off : a.dsrc_off) + b * w + c;
   const int str = a.B * w;
@@ -694,6 +697,14 @@ inline LayerK make_layer_k(const dgprf_plan_t& pl, const StepDev& sd, int l, int
     if (dgprf::agemm_parts(pl.batch, rows, pl.d_in, pl.d[0], pl.n_rf[0]) == 2)
       a.a0_sl = (int32_t)(rows * pl.n_rf[0]);
   }
+  // folded output layer (W-only backward of layer L): W_L [P] then Omega_L rows [d][R + 16] (the
+  // padding spreads the 4 k-rows a wave reads over distinct banks), after everything else
+  a.rcf = (bwd && a.last && pl.fold_out && !sd.full_bayes && nwb == 4) ? 1 : 0;
+  a.rcf_off = 0;
+  if (a.rcf) {
+    a.rcf_off = round4(lds_floats);
+    lds_floats = a.rcf_off + (a.kind_rbf ? 2 : 1) * a.R + a.d * (a.R + 16);
+  }
   a.rt_per_rg = 1;
   a.ncw = a.nrw = a.rg_fast = a.gred_off = a.rg_nit = 0;
   a.rw_one = a.cmp = 0;
@@ -753,6 +764,35 @@ inline bool step_fused_fwd(const dgprf_plan_t& pl) {
   return pl.rt_per_group >= 8 && pl.n_chains == 1 && pl.a0_off < 0;
 }
 
+// A-tile k-steps of the step kernels for input width d (the KS instance a layer runs)
+__host__ __device__ inline int step_ks(int d) { return d <= 4 ? 1 : (d <= 8 ? 2 : (d <= 16 ? 4 : 8)); }
+
+// Output layer folded into its backward ("recompute instead of synchronise"): for a g_L = 1
+// Gaussian output layer, every k_step_bwd workgroup of layer L recomputes F_L for its 16 rows over
+// all R_L features from the X tile it loads anyway (F_{L-1}), with the layer's whole W_L and
+// Omega_L staged in LDS, and forms dF_L (likelihoods/gaussian.py:18-25) in place — so the step has
+// no forward launch for layer L and no F_L slice partials.  The recompute is 16x that layer's
+// forward work (16 feature slices per row tile), so it is taken only where a launch boundary
+// costs more: B <= 256 (per-tile backward), fewer than 4 chains (one feature chunk per wave per
+// slice, the chip not full), and at most 128 A-tile k-steps per 4-wave workgroup ((R_L / 16) x
+// KS(d_L): config 2's 1,024-feature, d = 8 output layer; not config 3's 2,048 x d = 9, nor config
+// 5's 8,192).  W-only steps: a full-Bayes step keeps the forward launch (plan-independent choice
+// at enqueue time).  The element-owner prologue must apply (4 waves, d_L <= 28, g_{L-1} <= 16).
+inline bool step_fold_out(const dgprf_plan_t& pl) {
+#ifdef DGPRF_NO_FOLD  // A/B diagnostic build (scripts/ab_variants.sh), never the product library
+  return false;
+#endif
+  const int L = pl.n_layers - 1;
+  const int d = pl.d[L], R = pl.n_rf[L];
+  if (pl.rt_per_group != 1 || pl.n_chains >= 4 || pl.n_gp[L] != 1 ||
+      pl.likelihood != DGPRF_LIK_GAUSSIAN || (L == 0 && pl.a0_off >= 0) || pl.ws_chain >= (1 << 29))
+    return false;
+  if (d > 28 || (L > 0 && pl.n_gp[L - 1] > 16) || R % 256 != 0 || (R / 16) * step_ks(d) > 128)
+    return false;
+  const int P = pl.kind[L] == DGPRF_RBF ? 2 * R : R;
+  return (int64_t)(P + d * (R + 16)) * 4 <= 48 * 1024;
+}
+
 // Row-wave backward layout of layer l (step_bwdrw_impl.h; floats): false when the layer does not
 // fit it — it needs the fused forward's complete F_l (step_fused_fwd), >= 8 row tiles per group,
 // d <= 32, g <= 12, 4 or 8 chunks per slice and at most 8 gW accumulator tiles per wave.
@@ -760,8 +800,6 @@ struct RwCfg {
   int nch, nwv, wsa, osa, ost, wave0, wstride, hred, gred, total;
   int xst, dst, gpw, orows;  // X / dF tile row strides, W staging row width, staged Omega rows
 };
-// A-tile k-steps of the step kernels for input width d (the KS instance a layer runs)
-__host__ __device__ inline int step_ks(int d) { return d <= 4 ? 1 : (d <= 8 ? 2 : (d <= 16 ? 4 : 8)); }
 inline bool rw_config(const dgprf_plan_t& pl, int l, bool fb, RwCfg& c, int max_nwv = 16) {
   const int d = pl.d[l], g = pl.n_gp[l], cpw = pl.cpw[l];
   const int dxw = l > 0 ? pl.n_gp[l - 1] : 0;

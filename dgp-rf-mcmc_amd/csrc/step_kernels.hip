@@ -744,8 +744,10 @@ hipError_t launch_step_bwd(const dgprf_plan_t& pl, const StepDev& sd, int layer,
     else k_step_bwd_rg_launch2<0>(g, rbf, fb, c.nit, grid, lds, s, a);
     return hipGetLastError();
   }
-  // 8 waves per workgroup for W-only steps whose slices are staged whole (a.wstage)
-  bool w8 = !sd.full_bayes && pl.cpw[layer] % 4 == 0;
+  // 8 waves per workgroup for W-only steps whose slices are staged whole (a.wstage); a folded
+  // output layer runs the 4-wave instance that recomputes F_L
+  const bool fold = pl.fold_out && !sd.full_bayes && layer == pl.n_layers - 1;
+  bool w8 = !sd.full_bayes && pl.cpw[layer] % 4 == 0 && !fold;
   int lds_floats = 0;
   LayerK a = make_layer_k(pl, sd, layer, lds_floats, /*bwd=*/true, w8 ? 8 : 4);
   if (w8 && !a.wstage) {  // the slice image does not fit next to 8 waves' rows: 4 waves
@@ -753,6 +755,8 @@ hipError_t launch_step_bwd(const dgprf_plan_t& pl, const StepDev& sd, int layer,
     lds_floats = 0;
     a = make_layer_k(pl, sd, layer, lds_floats, /*bwd=*/true, 4);
   }
+  // the step launched no forward for a folded output layer: its backward must recompute F_L
+  if (fold && !(a.rcf && a.fast)) return hipErrorInvalidValue;
 #ifdef DGPRF_STAMPS
   a.stamps = rg_stamp_buffer();
 #endif

@@ -22,7 +22,7 @@ RNG_NOISE, RNG_RESAMPLE, RNG_Z, RNG_W, RNG_MOMENTS = 1, 2, 3, 4, 5
 RNG_HYPER, RNG_HYPER_RESAMPLE = 6, 7
 HYP_KERNEL, HYP_LIK, HYP_MEAN = 1, 2, 4
 HMASS = 32  # hmass slots: log_amp l -> l, log_inv_ls l -> 8 + l, mean l -> 16 + l, lik_log_var -> 24
-ABI_VERSION = 9
+ABI_VERSION = 10
 FWD_AUTO, FWD_ROWS, FWD_NO_AGEMM, FWD_TILE, FWD_ROWS16, FWD_ROWS8 = 0, 1, 2, 3, 4, 5
 
 E_ARG, E_SHAPE, E_HIP, E_PLAN = -1, -2, -3, -4
@@ -46,7 +46,7 @@ class Plan(ctypes.Structure):
         ("initialised", _i32),
         ("d", _i32 * _L), ("P", _i32 * _L), ("ns", _i32 * _L), ("cpw", _i32 * _L),
         ("n_row_tiles", _i32), ("n_rt_pad", _i32), ("rt_per_group", _i32), ("n_gw_rows", _i32),
-        ("rg_full_bayes", _i32), ("pad1", _i32),
+        ("rg_full_bayes", _i32), ("fold_out", _i32),
         ("omega_off", _i64 * _L), ("w_off", _i64 * _L), ("lis_off", _i64 * _L),
         ("mean_off", _i64 * _L), ("fp_off", _i64 * _L), ("dxp_off", _i64 * _L),
         ("gwp_off", _i64), ("logp_off", _i64),

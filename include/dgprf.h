@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define DGPRF_ABI_VERSION 9
+#define DGPRF_ABI_VERSION 10
 
 #define DGPRF_MAX_LAYERS 8
 #define DGPRF_MAX_G 64        /* max latent GPs per layer (n_gp[l]) */
@@ -147,7 +147,13 @@ typedef struct dgprf_plan {
   int32_t rg_full_bayes;            /* rt_per_group > 1: every layer also fits the full-Bayes
                                        row-group backward (else full_bayes steps / gradients
                                        return DGPRF_E_SHAPE for this batch size)                */
-  int32_t pad1;
+  int32_t fold_out;                 /* 1: W-only steps fold the output layer's forward into its
+                                       backward — every backward workgroup of layer L recomputes
+                                       its 16 rows of F_L over all R_L features instead of summing
+                                       the 16 slice partials of a separate forward launch (one
+                                       launch and one dependent boundary fewer per step; g_L = 1
+                                       Gaussian output layers with a small d_L R_L, B <= 256,
+                                       fewer than 4 chains); ABI 10 */
   int64_t omega_off[DGPRF_MAX_LAYERS];
   int64_t w_off[DGPRF_MAX_LAYERS];
   int64_t lis_off[DGPRF_MAX_LAYERS];

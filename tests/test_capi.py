@@ -28,7 +28,7 @@ def test_exports_every_declared_symbol():
     for n in names:
         assert hasattr(lib, n), n
     assert set(names) == set(N.SIGNATURES), set(names) ^ set(N.SIGNATURES)
-    assert lib.dgprf_abi_version() == N.ABI_VERSION == 9
+    assert lib.dgprf_abi_version() == N.ABI_VERSION == 10
 
 
 def test_struct_layout_matches_c(tmp_path):
@@ -101,3 +101,20 @@ def test_row_group_workspace_bounded():
         assert pl.n_gw_rows == rows, (B, pl.n_gw_rows)
         assert pl.n_rt_pad == 16
         assert (pl.rt_per_group > 1) == (B > 256)
+
+
+def test_fold_out_plan_choice():
+    """Which plans fold the output layer (host-only plan derivation): config 2 at B = 200 with 1-3
+    chains; not from 4 chains (wider slices, the chip full of chains), not past B = 256 (row-group
+    backward), not configs 3 / 5 (recompute costlier than the boundary) nor softmax outputs."""
+    from dgprf import _native as N
+    RBFk, ARCk = N.RBF, N.ARC
+    mk = lambda kinds, R, g, D, B, C=1, lik=N.LIK_GAUSSIAN: N.make_plan(
+        D, g[-1], kinds, R, g, False, lik, B, C)
+    assert mk([RBFk] * 3, [1024] * 3, [8, 8, 1], 8, 200).fold_out == 1
+    assert mk([RBFk] * 3, [1024] * 3, [8, 8, 1], 8, 200, C=3).fold_out == 1
+    assert mk([RBFk] * 3, [1024] * 3, [8, 8, 1], 8, 200, C=4).fold_out == 0
+    assert mk([RBFk] * 3, [1024] * 3, [8, 8, 1], 8, 1024).fold_out == 0
+    assert mk([ARCk] * 3, [2048] * 3, [9, 9, 1], 9, 200).fold_out == 0
+    assert mk([RBFk, ARCk, RBFk, ARCk, RBFk], [8192] * 5, [16] * 4 + [1], 16, 200).fold_out == 0
+    assert mk([RBFk] * 2, [1024] * 2, [8, 10], 8, 200, lik=N.LIK_SOFTMAX).fold_out == 0

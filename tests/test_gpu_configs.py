@@ -660,3 +660,50 @@ def test_full_bayes_graph_replay_invalidates_projection(dev):
     ref = Xt.double() @ eng.omega_view(0).double()
     assert float((now[:500].double() - ref).abs().max()) <= 2e-5 * float(ref.abs().max())
     assert not torch.equal(now[:500], before[:500])  # Omega_1 did move
+
+
+# ------------------------------------------------------------------ folded output layer
+@pytest.mark.parametrize("kinds,n_rf,n_gp,D,B", [
+    (["RBF"] * 3, [1024] * 3, [8, 8, 1], 8, 200),   # config 2 at its benchmarked B
+    (["RBF"] * 3, [1024] * 3, [8, 8, 1], 8, 19),    # one ragged row tile
+    (["RBF", "ARC"], [512, 512], [6, 1], 5, 77),    # ARC output layer (relu features)
+    (["RBF"], [256], [1], 12, 50),                  # one layer: the folded layer reads X itself
+])
+def test_folded_output_layer_grad_and_step(dev, kinds, n_rf, n_gp, D, B):
+    """plan.fold_out (step_fold_out): the output layer's forward is not launched; every backward
+    workgroup of layer L recomputes its rows of F_L from the staged W_L / Omega_L.  Gradients of
+    every layer against the float64 oracle, one injected-noise SGHMC step against the oracle's
+    update, and the same gradient from a 4-chain engine (fold off: the forward launch and its 16
+    slice partials) to fp32 rounding of the other summation order."""
+    from dgprf import engine as E
+    c = dict(kinds=kinds, n_rf=n_rf, n_gp=n_gp, D=D, lik="gaussian")
+    m, p = _model(c, 90 + B)
+    eng = m._engine
+    L = len(kinds)
+    pl, _ = eng.plan_ws(B)
+    assert pl.fold_out == 1
+    X, Y = _data(c, B, 91 + B)
+    N_ = 50_000
+    G = eng.grad(X, Y, N_)
+    ref = O.grad_W(p, X, Y, N_)
+    for l in range(L):
+        assert rel_err(unpack(eng, G)[l], ref[l]) < 1e-4, ("grad", l)
+    four = E.Engine(eng.spec, 4, seed=eng.seed)
+    assert four.plan_ws(B)[0].fold_out == 0
+    four.z.copy_(eng.z)
+    four.hyp.copy_(eng.hyp)
+    four.theta.copy_(eng.theta.expand(4, -1))
+    four.lik_log_var_source = eng.lik_log_var_source
+    four.build_omega()
+    G4 = four.grad(X, Y, N_)
+    for l in range(L):
+        assert rel_err(unpack(four, G4)[l], unpack(eng, G)[l]) < 2e-5, ("4 chains", l)
+    rng = np.random.default_rng(B)
+    m.precond_update(None, N_, precond_type="identity")
+    m0 = [cpu(eng.mom_view(l)).astype(np.float64) for l in range(L)]
+    xi = [rng.standard_normal(w.shape) for w in p.W]
+    eng.step(X, Y, N_, 0.01, 0.9, 1.0, xi=pack(eng, xi))
+    O.sgmcmc_step(p, m0, X, Y, N_, 0.01, 0.9, 1.0, [1.0] * L, xi)
+    for l in range(L):
+        assert rel_err(cpu(eng.W_view(l)), p.W[l]) < 2e-5, ("step", l)
+
