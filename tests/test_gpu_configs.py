@@ -611,9 +611,15 @@ def test_dataset_a1_same_address_new_dataset(dev):
     m = DGP_RF(100, 5, n_hidden_layers=2, n_rf=[256, 128], n_gp=[10, 5], likelihood=Softmax(),
                kernel_type_list=["RBF", "RBF"])
     eng = m._engine
-    ptrs = []
+    ptrs, spare = [], []
     for seed in (1, 2):
-        Xt = torch.rand(3000, 100, device=dev) * 2 - 1 + 0.1 * seed
+        Xt = torch.empty(3000, 100, device=dev)
+        for _ in range(8):  # the second set: until the allocator hands out the first one's block
+            if not ptrs or Xt.data_ptr() == ptrs[0]:
+                break
+            spare.append(Xt)
+            Xt = torch.empty(3000, 100, device=dev)
+        Xt.uniform_(-1 + 0.1 * seed, 1 + 0.1 * seed)
         Yt = torch.randint(0, 5, (3000, 1), device=dev).float()
         ptrs.append(Xt.data_ptr())
         acc = PredictiveLSE(eng, Xt, Yt)
@@ -628,6 +634,7 @@ def test_dataset_a1_same_address_new_dataset(dev):
         assert len(eng._a1_cache) == 1
         del acc, ref, Xt, Yt
         gc.collect()
+        torch.cuda.synchronize()
         assert not eng._a1_cache  # the finaliser dropped the freed dataset's projection
     assert ptrs[0] == ptrs[1], "allocator did not reuse the block: the case is not exercised"
 

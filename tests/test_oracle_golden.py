@@ -119,3 +119,21 @@ def test_predictive_summary(golden):
     lp = g["logp"] - np.log(float(g["y_std"]))
     direct = np.mean(np.log(np.mean(np.exp(lp), axis=0)))
     assert np.isclose(ll, direct)
+
+
+def test_demo_square_printed_kernel_values():
+    """train_regression_demo_square.ipynb prints length_scale [1.4142137] (cell 5, :195) and
+    amplitude 0.5 (cell 6, :215) for its model's RBF kernel.  Its DemoRegressionDGP class is not in
+    the reference's code, so what is pinned here is the kernel arithmetic that
+    produces those values (kernels/RBF.py:15-17,39-53): the default length scale sqrt(d) of a d = 2
+    input, stored as log(1 / l) in float32 and read back through exp — to within one float32 ulp of
+    the printout (TF's float32 exp / log and the host's round differently by an ulp) — and an
+    amplitude of 0.5 stored as its log and read back exactly."""
+    from kernels import RBFKernel
+    printed = np.float32(1.4142137)
+    ulp = np.spacing(printed)
+    assert abs(np.float32(np.exp(-O.init_log_inv_ls(2)[0])) - printed) <= ulp
+    k = RBFKernel(2, is_ard=True)
+    ls = k.length_scale.detach().cpu().numpy().astype(np.float32)
+    assert ls.shape == (2,) and np.all(np.abs(ls - printed) <= ulp)
+    assert float(RBFKernel(1, amplitude=0.5).amplitude) == 0.5
