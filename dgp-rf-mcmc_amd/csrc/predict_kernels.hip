@@ -525,8 +525,6 @@ constexpr int TILE_WAVES = 4;       // waves per SIMD the register budget must a
 constexpr int TILE_TPW_DEFAULT = 1; // 16-row tiles per wave (2: two chains per wave, but 186 VGPRs ->
                                     // 2 waves/SIMD, slower)
 constexpr bool TILE_APHASE = true;  // issue a block's four A-tile chains before its trig / F work
-constexpr int TILE_PAIR_WAVES = 5;  // pair kernel budget (A/B)
-
 constexpr int TILE_LEAN_WAVES = 5;  // waves per SIMD of the lean instance (NOTMAX = 0, every layer
                                     // g, d <= 8); it computes each chunk's A tile just before use
                                     // (the A-phase there measured slower: 225 vs 213 us)
@@ -981,180 +979,6 @@ __device__ __forceinline__ void tile_layer0_pair(const dgprf_plan_t& pl, const f
   __syncthreads();  // both samples' F tiles complete before layer 1 reads its x fragments
 }
 
-// Layer l >= 1 of a PAIR of samples (pair kernel, lean models: d_l, g_l <= 8), both samples in one
-// instruction stream.  The samples share Omega_l (z fixed, layers/rf_layers.py:21-22) but not their
-// inputs (F_{l-1} of each sample) nor W_l, so the 16 MFMA rows are MIXED: lane row j = 8 s + r is
-// tile row 8 p + r of sample s, pass p = 0, 1 covering the tile's rows 0-7 and 8-15.  One A = X Omega
-// chain and one cos / sin per mixed row serve both samples; for 2 <= g <= 8 the F contraction runs
-// on v_mfma_f32_16x16x4_f32 with output row i = 8 s + o (the two samples' W_l side by side, staged
-// as in tile_layer0_pair) and column j = 8 s' + r: the diagonal blocks s = s' are the samples' F,
-// the off-diagonal half is discarded — still twice the useful MACs per SIMD issue slot of the
-// one-sample 4x4x1 blocks (16 instead of 32 issue slots of ~8 cycles per 16-feature chunk for
-// the pair), and the two samples' dependency chains are interleaved in every chunk.  g == 1: a VALU
-// dot product with each lane's own sample's W_l.  Per-row sums over the features run in the same
-// order as the one-sample body's (features 4 lq + r of each chunk, chunks in order, then the four
-// feature groups); the MFMA accumulation groups them differently, so results agree to fp32
-// rounding, not bits.
-template <bool RBF, bool G1>
-__device__ __forceinline__ void tile_layer_pairmix(const dgprf_plan_t& pl, int layer,
-                                                   const float* __restrict__ W0,
-                                                   const float* __restrict__ W1,
-                                                   const float* __restrict__ om, float cl,
-                                                   const TileLds& T, float* smem, const float* xin,
-                                                   float* ftw0, float* ftw1, int lr, int lq) {
-  constexpr int KS = 2;
-  constexpr bool REV = RBF && !DGPRF_PRECISE_TRIG_ON;
-  const int d = pl.d[layer], R = pl.n_rf[layer], g = pl.n_gp[layer];
-  const int gp = pl.n_gp[layer - 1];
-  int tid = threadIdx.x;
-  asm volatile("" : "+v"(tid));  // per-layer lane offsets (see tile_layer's OPQ)
-  lr = tid & 15;
-  lq = (tid & 63) >> 4;
-  const int sl = lr >> 3, rl = lr & 7;  // this lane's column: sample sl, row 8 p + rl
-  const float* fin = sl ? ftw1 : ftw0;
-  float xf[2][KS];
-#pragma unroll
-  for (int p = 0; p < 2; ++p)
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      const int col = 4 * ks + lq, row = 8 * p + rl;
-      const float a = fin[row * T.ftst + min(col, T.ftst - 1)];
-      const float b = xin[row * T.xin_st + min(max(col - gp, 0), T.xin_st - 1)];
-      xf[p][ks] = col < gp ? a : (col < d ? b : 0.f);
-    }
-  const int gmag = (1048576 + g - 1) / g;
-  const int64_t wn = (int64_t)(RBF ? 2 : 1) * R * g, sd1 = (int64_t)(W1 - W0);
-  const rsrc_t rw = make_rsrc(W0, sd1 + wn);
-  const rsrc_t ro = make_rsrc(om, (int64_t)d * R);
-  const int nh4 = 16 * g;  // float4 of one half's 64-feature block of one sample
-  f4 sw[2], so;
-  auto stage_load = [&](int fb) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {  // i < 2 samples x (RBF ? 2 : 1) halves x 16 g
-      const int i = tid + 256 * j, sidx = i >= 2 * nh4, q = i - sidx * 2 * nh4, h = q >= nh4;
-      const int e4 = q - h * nh4;
-      const bool ok = (RBF || h == 0) && i < 4 * nh4;
-      const uint32_t off = (uint32_t)((sidx * sd1 + ((h * R) + fb) * g + 4 * e4) * 4);
-      sw[j] = bload4(rw, ok ? off : DGPRF_OOB);
-    }
-    const int k = tid >> 4, c4 = tid & 15;
-    so = bload4(ro, k < d && fb + 4 * c4 < R ? (uint32_t)((k * R + fb + 4 * c4) * 4) : DGPRF_OOB);
-  };
-  // W rings: g > 1 [h][64][PST] with sample s at columns 8 s + o (tile_layer0_pair's layout);
-  // g == 1 [s][h][64].  Feature rows >= R are zeroed.
-  auto stage_store = [&](int buf, int fb) {
-    float* wsb = smem + T.w_off + buf * T.wbuf;
-    float* osb = smem + T.o_off + buf * T.obuf;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int i = tid + 256 * j, sidx = i >= 2 * nh4, q = i - sidx * 2 * nh4, h = q >= nh4;
-      const int e0 = 4 * (q - h * nh4);
-      if ((RBF || h == 0) && i < 4 * nh4) {
-        if (G1) {
-          f4 v = sw[j];
-#pragma unroll
-          for (int t = 0; t < 4; ++t) v[t] = fb + e0 + t < R ? v[t] : 0.f;
-          *reinterpret_cast<f4*>(wsb + (2 * sidx + h) * 64 + e0) = v;
-        } else {
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            const int e = e0 + t, row = (e * gmag) >> 20, col = e - row * g;
-            if (row < 64) wsb[(h * 64 + row) * PST + 8 * sidx + col] = fb + row < R ? sw[j][t] : 0.f;
-          }
-        }
-      }
-    }
-    if ((tid >> 4) < T.orows)
-      *reinterpret_cast<f4*>(osb + (tid >> 4) * TW_OST + 4 * (tid & 15)) =
-          REV ? so * 0.15915494309189535f : so;
-  };
-  f4 acc[2], acs[2];
-  float dot[2] = {0.f, 0.f};
-#pragma unroll
-  for (int p = 0; p < 2; ++p) acc[p] = acs[p] = f4zero();
-  const int nb = (R + 63) >> 6;
-  stage_load(0);
-  stage_store(0, 0);
-  __syncthreads();
-  for (int blk = 0; blk < nb; ++blk) {
-    const int fb = blk * 64, buf = blk & 1;
-    if (blk + 1 < nb) stage_load(fb + 64);
-    const float* wsb = smem + T.w_off + buf * T.wbuf;
-    const float* wl = wsb + (G1 ? sl * 128 + 4 * lq : 4 * lq * PST + lr);
-    const float* osb = smem + T.o_off + buf * T.obuf + lq * TW_OST + lr;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      float omk[KS];
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) omk[ks] = osb[4 * ks * TW_OST + 16 * c];
-      // A[mixed row lr][feature fb + 16 c + 4 lq + r], pass by pass (the two passes' chains are
-      // independent; one pass's A tile / features live at a time keeps the lean register budget)
-#pragma unroll
-      for (int p = 0; p < 2; ++p) {
-        f4 at = f4zero();
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) at = mfma16(omk[ks], xf[p][ks], at);
-        float p0[4], p1[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          if (REV) {
-            const float u = __builtin_amdgcn_fractf(at[r]);
-            p0[r] = __builtin_amdgcn_cosf(u);
-            p1[r] = __builtin_amdgcn_sinf(u);
-          } else if (RBF) {
-            float sv, cv;
-            rf_sincos(at[r], &sv, &cv);
-            p0[r] = cv;
-            p1[r] = sv;
-          } else {
-            p0[r] = fmaxf(at[r], 0.f);
-            p1[r] = 0.f;
-          }
-        }
-        if (G1) {
-          const f4 w0 = *reinterpret_cast<const f4*>(wl + 16 * c);
-          const f4 w1 = RBF ? *reinterpret_cast<const f4*>(wl + 64 + 16 * c) : f4zero();
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            dot[p] = fmaf(p0[r], w0[r], dot[p]);
-            if (RBF) dot[p] = fmaf(p1[r], w1[r], dot[p]);
-          }
-        } else {
-          // F^T[i = 8 s + o][j] += W_s[feature][o] Phi[mixed row j][feature], K = the 4 features
-          // of k-step r
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            acc[p] = mfma16(wl[(16 * c + r) * PST], p0[r], acc[p]);
-            if (RBF) acs[p] = mfma16(wl[(64 + 16 * c + r) * PST], p1[r], acs[p]);
-          }
-        }
-      }
-    }
-    if (blk + 1 < nb) stage_store(buf ^ 1, fb + 64);
-    __syncthreads();
-  }
-  float* fo = sl ? ftw1 : ftw0;
-  if (G1) {
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      float v = dot[p];
-      v += __shfl_xor(v, 16);
-      v += __shfl_xor(v, 32);
-      if (lq == 0) fo[(8 * p + rl) * T.ftst] = cl * v;
-    }
-  } else if ((lq >> 1) == sl) {
-    // acc[p][rr] = F[i = 4 lq + rr][j = lr] / c: the diagonal block of sample sl, o = 4 (lq & 1) + rr
-#pragma unroll
-    for (int p = 0; p < 2; ++p)
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int o = 4 * (lq & 1) + rr;
-        if (o < g) fo[(8 * p + rl) * T.ftst + o] = cl * (acc[p][rr] + acs[p][rr]);
-      }
-  }
-  __syncthreads();  // both samples' F tiles complete before the next layer reads them
-}
-
 // Per-wave timeline of the tile kernel for a separate diagnostic build (-DDGPRF_PSTAMPS, never in
 // the product): slot 0 = s_memrealtime at entry, 7 = s_memtime at entry, 1..4 = s_memtime after
 // each layer, 6 = s_memrealtime at exit, 5 = HW_ID | XCC_ID << 32.
@@ -1311,7 +1135,7 @@ void k_forward_tiles(
 // chain's online log-sum-exp accumulators in sample order (experiments/utils_training.py:79-85).
 // A workgroup covers 64 test rows of one chain, so each accumulator element has one writer.
 // Same register budget as the lean one-sample instance.
-__global__ __launch_bounds__(TW_THREADS) __attribute__((amdgpu_waves_per_eu(TILE_PAIR_WAVES)))
+__global__ __launch_bounds__(TW_THREADS) __attribute__((amdgpu_waves_per_eu(TILE_LEAN_WAVES)))
 void k_forward_pairs(const dgprf_plan_t pl, const float* __restrict__ thetas, const int n_samples,
                      const float* __restrict__ omega, const float* __restrict__ der,
                      const float* __restrict__ X, const float* __restrict__ Y, const int y_cols,
@@ -1352,27 +1176,26 @@ void k_forward_pairs(const dgprf_plan_t pl, const float* __restrict__ thetas, co
     else
       tile_layer0_pair<false>(pl, W0, W1, om0, der[dchain], T, smem, xin, ftw0, ftw1, lr, lq);
     DGPRF_PST(1, PST_CLK());
-    // layers >= 1: both samples in one instruction stream (mixed rows; an odd last sample runs as
-    // its own pair, the second copy discarded)
-    for (int layer = 1; layer < L; ++layer) {
-      const float* __restrict__ om = omega + ochain + pl.omega_off[layer];
-      const float cl = der[dchain + layer];
-      const bool rbf = pl.kind[layer] == DGPRF_RBF;
-      const float* Wa = W0 + pl.w_off[layer];
-      const float* Wb = W1 + pl.w_off[layer];
-      if (pl.n_gp[layer] == 1) {
-        if (rbf) tile_layer_pairmix<true, true>(pl, layer, Wa, Wb, om, cl, T, smem, xin, ftw0, ftw1, lr, lq);
-        else tile_layer_pairmix<false, true>(pl, layer, Wa, Wb, om, cl, T, smem, xin, ftw0, ftw1, lr, lq);
-      } else {
-        if (rbf) tile_layer_pairmix<true, false>(pl, layer, Wa, Wb, om, cl, T, smem, xin, ftw0, ftw1, lr, lq);
-        else tile_layer_pairmix<false, false>(pl, layer, Wa, Wb, om, cl, T, smem, xin, ftw0, ftw1, lr, lq);
-      }
-    }
-    DGPRF_PST(2, PST_CLK());
+    // unrolled: each sample's copy of layers >= 1 keeps only its own state live (a loop over the
+    // two samples spilled 5 VGPRs at the 96-register budget; unrolled: 92, none spilled)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       if (j == 1 && !two) break;
       float* ftw = j ? ftw1 : ftw0;
+      const float* Wc = j ? W1 : W0;
+      for (int layer = 1; layer < L; ++layer) {
+        const float* __restrict__ om = omega + ochain + pl.omega_off[layer];
+        const float* __restrict__ W = Wc + pl.w_off[layer];
+        const float cl = der[dchain + layer];
+        const bool rbf = pl.kind[layer] == DGPRF_RBF;
+        if (pl.n_gp[layer] == 1) {
+          if (rbf) tile_layer<1, true, true, false, 1, 1, 2, 1, false, true>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, n, nullptr);
+          else tile_layer<1, false, true, false, 1, 1, 2, 1, false, true>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, n, nullptr);
+        } else {
+          if (rbf) tile_layer<1, true, false, true, 1, 1, 2, 1, false, true>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, n, nullptr);
+          else tile_layer<1, false, false, true, 1, 1, 2, 1, false, true>(pl, layer, W, om, cl, T, smem, xin, ftw, lr, lq, wrow0, n, nullptr);
+        }
+      }
       // likelihood of this sample, folded into the chain's accumulators (as k_forward_tiles)
       const int64_t b = wrow0 + lr;
       if (lq == 0 && b < n) {
@@ -1406,8 +1229,8 @@ void k_forward_pairs(const dgprf_plan_t pl, const float* __restrict__ thetas, co
           lse_fold1(lse_m, lse_s, se_sum, idx, lp, se);
         }
       }
+      DGPRF_PST(2 + j, PST_CLK());
     }
-    DGPRF_PST(3, PST_CLK());
   }
   DGPRF_PST(6, __builtin_amdgcn_s_memrealtime());
 }

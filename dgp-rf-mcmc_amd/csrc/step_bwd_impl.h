@@ -67,24 +67,35 @@ __device__ __forceinline__ float rcf_row_partial(const LayerK& a, const float* s
   const float* wl = smem + a.rcf_off;
   const float* ol = wl + (RBF ? 2 * R : R);
   float acc = 0.f;
-  for (int c = wave; c < nch; c += 4) {
-    const int f0 = c * 16;
-    f4 at = f4zero();
+  // four chunks per group (c0, c0 + 4, c0 + 8, c0 + 12: R % 256 == 0, so every wave's chunk count
+  // is a multiple of 4): their A-tile chains are issued together, then the four chunks' features
+  // and dot products — independent dependency chains for one wave per SIMD to overlap
+  for (int c0 = wave; c0 < nch; c0 += 16) {
+    f4 at[4];
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      const int k = 4 * ks + lq;
-      const float o = ol[(k < d ? k : d - 1) * ost + f0 + lr];  // rows >= d: not staged
-      at = mfma16(k < d ? o : 0.f, xf[ks], at);  // at[r] = A[row lr][f0 + 4 lq + r]
+    for (int q = 0; q < 4; ++q) {
+      const int f0 = (c0 + 4 * q) * 16;
+      at[q] = f4zero();
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int k = 4 * ks + lq;
+        const float o = ol[(k < d ? k : d - 1) * ost + f0 + lr];  // rows >= d: not staged
+        at[q] = mfma16(k < d ? o : 0.f, xf[ks], at[q]);  // at[r] = A[row lr][f0 + 4 lq + r]
+      }
     }
-    float p0[4], p1[4];
-    features<RBF>(at, cl, p0, p1);
-    const f4 w0 = *reinterpret_cast<const f4*>(wl + f0 + 4 * lq);
-    f4 w1 = f4zero();
-    if (RBF) w1 = *reinterpret_cast<const f4*>(wl + R + f0 + 4 * lq);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      acc = fmaf(p0[r], w0[r], acc);
-      if (RBF) acc = fmaf(p1[r], w1[r], acc);
+    for (int q = 0; q < 4; ++q) {
+      const int f0 = (c0 + 4 * q) * 16;
+      float p0[4], p1[4];
+      features<RBF>(at[q], cl, p0, p1);
+      const f4 w0 = *reinterpret_cast<const f4*>(wl + f0 + 4 * lq);
+      f4 w1 = f4zero();
+      if (RBF) w1 = *reinterpret_cast<const f4*>(wl + R + f0 + 4 * lq);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        acc = fmaf(p0[r], w0[r], acc);
+        if (RBF) acc = fmaf(p1[r], w1[r], acc);
+      }
     }
   }
   acc += __shfl_xor(acc, 16);

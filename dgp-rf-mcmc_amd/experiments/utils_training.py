@@ -8,7 +8,8 @@ Same functions, signatures, schedule and sample bookkeeping as the reference:
 
 Per epoch the reference runs precond_update, then one sgmcmc_update per minibatch with lr_0 and
 T = 0 during burn-in and lr_0 * cyclical_step_rate(...)^2, T = 1 afterwards, scoring the test set at
-the end of each cycle.  Here a whole epoch of steps is ONE hipGraph replay: minibatches are drawn
+the end of each cycle.  Here an epoch of steps is a few replays of one captured hipGraph (at most
+EPOCH_GRAPH_STEPS steps each): minibatches are drawn
 on the device (per-epoch permutation, drop remainder), and the burn-in / cosine schedule and the
 cycle-head momentum resampling are evaluated inside the update kernel from the device step counter
 (DGPRF_SCHED_CYCLICAL, the same float32 formula as utils.py:49-73 with min_value = 0).  The host
@@ -28,6 +29,9 @@ from experiments.utils_dataset import (DeviceDataset, download_UCI_data_info, lo
 from utils import cyclical_step_rate
 
 REFERENCE_SAMPLE_ALIASING = False
+# steps per captured graph of an epoch: config 2's 5,000-step epoch as one 5,000-step graph ran
+# 30.9 us/step against 27.9 for replays of a 100-step graph (bench.py `driver`, same box)
+EPOCH_GRAPH_STEPS = 100
 
 
 def _store_W(model):
@@ -61,10 +65,14 @@ def _run_epochs(model, ds_train, ds_M, data_size, batch_size, lr_0, momentum_dec
                              precond_type=precond_type,
                              second_moment_centered=second_moment_centered)
         if graph:
+            # the epoch as replays of one graph of at most EPOCH_GRAPH_STEPS steps (the schedule
+            # and minibatch position come from the device step counter, so a graph replays
+            # anywhere in the epoch)
             model.run_sgmcmc(ds_train.X, ds_train.Y, data_size, iterations_per_epoch,
                              batch_size=ds_train.batch_size, lr=lr_0,
                              momentum_decay=momentum_decay, temperature=1.,
-                             steps_per_graph=iterations_per_epoch, perm_seed=ds_train.seed,
+                             steps_per_graph=min(iterations_per_epoch, EPOCH_GRAPH_STEPS),
+                             perm_seed=ds_train.seed,
                              schedule='cyclical',
                              start_step=t0 + start_sampling_epoch * iterations_per_epoch,
                              cycle_length=cycle_length,
