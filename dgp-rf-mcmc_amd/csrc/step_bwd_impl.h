@@ -237,12 +237,15 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
     // folded output layer: F_L of this row tile from the X tile (F_{L-1}) and the staged layer,
     // the 4 waves' feature shares summed in wave order into the dF tile (rows >= B: 0)
     __syncthreads();  // X tile, Y values and the LDS copies of W_L / Omega_L
+    STEP_STAMP(stamp_base, 5);
     float xr[8];
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) xr[ks] = (ks < KS && 4 * ks < d) ? xs[lr * a.xst + 4 * ks + lq] : 0.f;
     const float v = rcf_row_partial<KS, RBF>(a, smem, xr, cl, wave, lr, lq);
+    STEP_STAMP(stamp_base, 7);
     if (lq == 0) red[wave * TR + lr] = v;
     __syncthreads();
+    STEP_STAMP(stamp_base, 10);
     if (threadIdx.x < TR) {
       const int r = threadIdx.x;
       const float f = ((red[r] + red[TR + r]) + red[2 * TR + r]) + red[3 * TR + r];
