@@ -196,7 +196,6 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
   const float* yr = a.yrows + (int64_t)chain * a.yrow_cs;
   float* ysh = dfs + round4(TR * dfst);
   const int yc = a.likelihood == DGPRF_LIK_GAUSSIAN ? g : 1;
-  if (RCF) rcf_stage<RBF>(a, W, om, smem);  // the whole output layer, for the F_L recompute
   if (a.fast) {
     // ---- single burst: W/Omega block, X tile, dF (or F_L) partials and Y rows
     f4 sw[2], so;
@@ -214,7 +213,11 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
       so = bload4(ro, k < dxw && fb0 + 4 * c4 < R ? (uint32_t)((k * R + fb0 + 4 * c4) * 4) : DGPRF_OOB);
     }
     STEP_STAMP(stamp_base, 1);
-    elem_prologue(a, chain, row0, TR * g, xs, dfs, dfst, ysh, red);
+    if (RCF)  // the whole output layer for the F_L recompute, copied while the partials load
+      elem_prologue_mid(a, chain, row0, TR * g, xs, dfs, dfst, ysh, red,
+                        [&]() { rcf_stage<RBF>(a, W, om, smem); });
+    else
+      elem_prologue(a, chain, row0, TR * g, xs, dfs, dfst, ysh, red);
     if (!WST && dphi) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) *reinterpret_cast<f4*>(wsl + 4 * ((int)threadIdx.x + 256 * j)) = sw[j];

@@ -331,6 +331,25 @@ __device__ __forceinline__ void elem_prologue(const LayerK& a, int chain, int ro
   if (np + wave0 < total) elem_store(e1, xs, dfs, ysh, scratch + t, np);
 }
 
+// The same prologue with `mid()` run between issuing the loads and their sums (every thread calls
+// it: workgroups of <= 8 waves only) — the folded output layer issues its LDS copies of W_L /
+// Omega_L there, so they queue behind the partial-sum loads instead of delaying them.
+template <class Mid>
+__device__ __forceinline__ void elem_prologue_mid(const LayerK& a, int chain, int row0, int nd_tile,
+                                                  float* xs, float* dfs, int dfst, float* ysh,
+                                                  float* scratch, Mid mid) {
+  const int total = TR * round4(a.d) + nd_tile;
+  const int t = threadIdx.x;
+  const int np = (int)blockDim.x;  // <= 512
+  const int wave0 = __builtin_amdgcn_readfirstlane(t & ~63);
+  Elem e0, e1;
+  if (wave0 < total) elem_issue(a, chain, row0, t, nd_tile, dfst, e0);
+  if (np + wave0 < total) elem_issue(a, chain, row0, t + np, nd_tile, dfst, e1);
+  mid();
+  if (wave0 < total) elem_store(e0, xs, dfs, ysh, scratch + t, np);
+  if (np + wave0 < total) elem_store(e1, xs, dfs, ysh, scratch + t, np);
+}
+
 // Omega fragments: omk[ks] = Omega[4ks+lq][f0+lr] (zero outside the layer), KS k-steps.
 template <int KS>
 __device__ __forceinline__ void load_om_frag(const float* __restrict__ om, int R, int d, int f0,
