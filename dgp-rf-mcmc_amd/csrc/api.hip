@@ -277,9 +277,10 @@ int dgprf_plan_init(dgprf_plan_t* pl) {
   pl->n_gw_rows = (pl->n_row_tiles + pl->rt_per_group - 1) / pl->rt_per_group;
   pl->n_rt_pad = (pl->n_gw_rows + 15) / 16 * 16;
   // the update kernel addresses the gW partials with 32-bit buffer offsets
-  if ((int64_t)pl->n_rt_pad * pl->w_total >= ((int64_t)1 << 29)) return DGPRF_E_SHAPE;
+  const int64_t gw_ld = dgprf_sk::gw_row_stride(pl->w_total);
+  if ((int64_t)pl->n_rt_pad * gw_ld >= ((int64_t)1 << 29)) return DGPRF_E_SHAPE;
   pl->gwp_off = ws;
-  ws = align4(ws + (int64_t)pl->n_rt_pad * pl->w_total);
+  ws = align4(ws + (int64_t)pl->n_rt_pad * gw_ld);
   pl->logp_off = ws;
   ws = align4(ws + B);
   // full-Bayes partials of each backward workgroup: per input dim sum_b X (dA z^T), sum_b X

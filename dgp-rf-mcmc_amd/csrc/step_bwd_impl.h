@@ -337,7 +337,7 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
   // this row tile's gW partial row, stored write-through (sc1): 13 rows x w_total floats at B = 200
   // that would otherwise sit dirty in the XCD L2s when the launch ends (configs 4 / 5: 12.8 /
   // 13.6 MB per layer; measured config 5 103 -> 98 us/step, config 4 126 -> 124)
-  const rsrc_t rgw = make_rsrc(a.gwp + (int64_t)chain * a.ws_cs + (int64_t)rt * a.w_cs, a.w_cs);
+  const rsrc_t rgw = make_rsrc(a.gwp + (int64_t)chain * a.ws_cs + (int64_t)rt * a.gw_ld, a.w_cs);
   auto gw_store = [&](int64_t i, float v) { bstore1_wt(v, rgw, (uint32_t)(i * 4)); };
   auto gw_store4 = [&](int64_t i, f4 v) { bstore4_wt(v, rgw, (uint32_t)(i * 4)); };  // i % 4 == 0
   float* gst = smem + a.gst_off + wave * 2 * 16 * g;  // this wave's gW tile staging (g % 16 != 0)

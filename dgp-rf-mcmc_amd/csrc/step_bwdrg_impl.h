@@ -472,7 +472,7 @@ __global__ __launch_bounds__(64 * RG_WAVES) void k_step_bwd_rg(const LayerK a) {
   RG_STAMP(stamp_base, 6);
 
   // ---- the group's gW partial row: row-waves summed in order (LDS), then stored
-  float* gwp = a.gwp + (int64_t)chain * a.ws_cs + (int64_t)rg * a.w_cs;
+  float* gwp = a.gwp + (int64_t)chain * a.ws_cs + (int64_t)rg * a.gw_ld;
   constexpr int GSZ = G1 ? NIT * 2 * 64 : NIT * NOT * 2 * 256;  // floats per wave
   float* gred = smem + a.gred_off;
   if (nrw > 1) {

@@ -422,7 +422,7 @@ __global__ __launch_bounds__(64 * NWV) void k_step_bwd_rw(const LayerK a) {
     __syncthreads();
   }
   // every thread sums a strided share of the gW values in slot order and stores them
-  float* gwp = a.gwp + (int64_t)chain * a.ws_cs + (int64_t)rg * a.w_cs;
+  float* gwp = a.gwp + (int64_t)chain * a.ws_cs + (int64_t)rg * a.gw_ld;
   if (G1) {
     for (int e = threadIdx.x; e < NCH * 2 * 16; e += blockDim.x) {
       const int c = e / 32, h = (e / 16) & 1, fl = e & 15;  // lanes 0..15 hold features fl

@@ -39,6 +39,13 @@ constexpr int TR = DGPRF_TILE_ROWS;
 constexpr int NSM = DGPRF_NS_MAX;
 constexpr float LOG_2PI = 1.8378770664093453f;
 constexpr int OST = 68;  // LDS row stride of the staged Omega block (16B-aligned rows)
+// Row stride of the gW partial rows (floats): w_total plus this padding, so the rows a lane of the
+// update kernel reads (configs 4 / 5: w_total x 4 B = 0x320000 / 0x310000 apart) do not share
+// their low address bits
+#ifndef DGPRF_GW_PAD
+#define DGPRF_GW_PAD 0
+#endif
+__host__ __device__ inline int64_t gw_row_stride(int64_t w_total) { return w_total + DGPRF_GW_PAD; }
 
 __host__ __device__ __forceinline__ int round4(int x) { return (x + 3) & ~3; }
 
@@ -70,13 +77,13 @@ struct LayerK {
   float* fout;          // F_l partials [NSM][B][g]
   const float* dxnext;  // dX_{l+1} partials [NSM][B][g]        (backward, l < L-1)
   float* dxout;         // dX_l partials [NSM][B][dxw]           (backward, l > 0)
-  float* gwp;           // gW partials of W_l, row-tile stride w_cs (backward)
+  float* gwp;           // gW partials of W_l, row-tile stride gw_ld (backward)
   float* logp;          // per-row log p [B]                       (backward, last layer)
   const float* xrows;   // minibatch X rows [B][d_in] (chain stride xrow_cs)
   const float* yrows;   // minibatch Y rows [B][y_cols] (chain stride yrow_cs)
   const float* cptr;    // c_l
   const float* varptr;  // sigma^2
-  int64_t w_cs, ws_cs, xrow_cs, yrow_cs, om_cs, der_cs;
+  int64_t w_cs, ws_cs, xrow_cs, yrow_cs, om_cs, der_cs, gw_ld;
   int32_t d, R, g, gp, dxw, cpw, B, d_in, y_cols;
   int32_t last, likelihood, layer;
   int32_t xst, aux_off, auxst, red_off;
@@ -156,11 +163,12 @@ struct HypK {
 struct UpdK {
   float* theta;         // chain 0 (chain stride w_total)
   float* mom;
-  const float* gwp;     // gW partials base of chain 0 (chain stride ws_cs, row-tile stride w_total)
+  const float* gwp;     // gW partials base of chain 0 (chain stride ws_cs, row-tile stride gw_ld)
   const float* mass;
   const int64_t* step;
   int32_t w_total, n_rt, n_rt_pad, n_layers;
   int32_t lo[DGPRF_MAX_LAYERS], hi[DGPRF_MAX_LAYERS];
+  int32_t gw_ld, pad_g;  // gW partial row stride (gw_row_stride)
   uint64_t seed;
   int64_t ws_cs;
   int32_t step_offset, upd_blocks;
@@ -558,12 +566,12 @@ __device__ __forceinline__ void w_update_quad(const K& a, const int e0, const in
     gr = bload4(make_rsrc(a.grad_in + cw, a.w_total), off);
   } else {
     // sum the row-tile gW partials in a fixed order: groups of 16 independent loads
-    const rsrc_t rs = make_rsrc(a.gwp + (int64_t)chain * a.ws_cs, (int64_t)a.n_rt * a.w_total);
+    const rsrc_t rs = make_rsrc(a.gwp + (int64_t)chain * a.ws_cs, (int64_t)a.n_rt * a.gw_ld);
     f4 sacc = f4zero();
     for (int rt0 = 0; rt0 < a.n_rt_pad; rt0 += 16) {
       f4 v[16];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) v[j] = bload4(rs, (uint32_t)(((rt0 + j) * a.w_total + e0) * 4));
+      for (int j = 0; j < 16; ++j) v[j] = bload4(rs, (uint32_t)(((rt0 + j) * a.gw_ld + e0) * 4));
 #pragma unroll
       for (int j = 0; j < 16; ++j) sacc += v[j];
     }
@@ -640,6 +648,7 @@ inline LayerK make_layer_k(const dgprf_plan_t& pl, const StepDev& sd, int l, int
   a.om_cs = fresh ? pl.ws_chain : sd.om_cs;
   a.der_cs = sd.der_cs;
   a.w_cs = pl.w_total;
+  a.gw_ld = gw_row_stride(pl.w_total);
   a.ws_cs = pl.ws_chain;
   a.d = pl.d[l];
   a.R = pl.n_rf[l];

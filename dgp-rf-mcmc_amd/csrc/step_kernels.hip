@@ -769,7 +769,8 @@ hipError_t launch_step_bwd(const dgprf_plan_t& pl, const StepDev& sd, int layer,
 hipError_t launch_step_update(const dgprf_plan_t& pl, const StepDev& sd, const UpdateDev& ud,
                               const float* grad_in, hipStream_t s, bool gather_next,
                               bool advance) {
-  if (pl.w_total >= (int64_t)1 << 30 || (int64_t)pl.n_rt_pad * pl.w_total >= (int64_t)1 << 29)
+  if (pl.w_total >= (int64_t)1 << 30 ||
+      (int64_t)pl.n_rt_pad * gw_row_stride(pl.w_total) >= (int64_t)1 << 29)
     return hipErrorInvalidValue;  // 32-bit buffer offsets
   UpdK a;
   a.theta = sd.theta;
@@ -778,6 +779,8 @@ hipError_t launch_step_update(const dgprf_plan_t& pl, const StepDev& sd, const U
   a.mass = sd.mass;
   a.step = sd.step;
   a.w_total = (int32_t)pl.w_total;
+  a.gw_ld = (int32_t)gw_row_stride(pl.w_total);
+  a.pad_g = 0;
   a.n_rt = pl.n_gw_rows;  // gW partial rows (one per row tile, or per row group)
   a.n_rt_pad = pl.n_rt_pad;
   a.n_layers = pl.n_layers;
