@@ -280,8 +280,9 @@ def bench_config(cfg, dev, rank, world, barrier_sync, max_over_ranks, steps):
                    "us_per_step_all_chains": round(t8 * 1e6 / (reps * 50), 2)}
         del gph, me
     # S posterior samples (the chain's W at S successive steps) scored by ONE add_samples call:
-    # every sample in one launch of the predictive kernel (grid.z = sample), then the fold
-    S = 3 if cfg == 5 else 10
+    # every sample in one launch of the predictive kernel (grid.z = sample), then the fold; S = the
+    # reference driver's default sample count (60), config 5 (1e6 test rows, ~27 ms per sample) 3
+    S = 3 if cfg == 5 else 60
     th_all = [m._engine.theta.clone()]
     for _ in range(S - 1):
         m.run_sgmcmc(X, Y, n, 1, **run)
@@ -572,7 +573,10 @@ def main():
     ap.add_argument("--steps", type=int, default=10000)
     ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--steps-per-graph", type=int, default=100)
-    ap.add_argument("--pred-samples", type=int, default=40)
+    # posterior samples scored per predictive call: the count the reference's default driver
+    # collects, (total_epochs - start_sampling_epoch) / epochs_per_cycle = (5000 - 2000) / 50
+    # (experiments/utils_training.py:11-16, 62-67)
+    ap.add_argument("--pred-samples", type=int, default=60)
     ap.add_argument("--multi-chains", type=int, default=64)
     ap.add_argument("--full-bayes-steps", type=int, default=2000)
     ap.add_argument("--cpu-runs", type=int, default=5)

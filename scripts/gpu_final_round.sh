@@ -6,7 +6,7 @@
 # ends it.  PART=1: suite + bench evidence only; PART=2: the config / counter profiles only.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 R=$PWD
-TAG=${TAG:-r05}
+TAG=${TAG:-r06}
 O=$R/gpurun_out/final_$TAG
 P=$R/profiles/$TAG
 mkdir -p $O $P
@@ -35,7 +35,7 @@ for c in 4 5; do
   python3 $R/scripts/pmc_summary.py $P/pmc_traffic_step_config$c.csv $O/pmc${c}_FETCH_SIZE $O/pmc${c}_WRITE_SIZE > /dev/null || exit 7
 done
 # SQ counters of the predictive pair kernel (issue port / MFMA pipe)
-NAME=pred_pairs CMD="python3 $R/scripts/prof_predict.py --samples 40 --batch" bash scripts/gpu_pmc.sh \
+NAME=pred_pairs CMD="python3 $R/scripts/prof_predict.py --samples 60 --batch" bash scripts/gpu_pmc.sh \
   > $O/pmc_pred_pairs.log 2>&1 || { tail $O/pmc_pred_pairs.log; exit 8; }
 cp $R/gpurun_out/pmc_pred_pairs/summary.csv $P/pmc_sq_predictive_pairs.csv
 cp $P/* $O/ 2>/dev/null
