@@ -1,14 +1,14 @@
 #!/bin/bash
-# GPU check: the GPU test suite, then (only if it is green) a bench run.
-#   TAG=... PYTEST_ARGS="-k ..." BENCH_ARGS="..." scripts/gpu_check.sh
+# Working check: targeted tests first, then the GPU suite, the fold A/B and a bench run.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
-O=gpurun_out/${TAG:-r4}
+O=gpurun_out/${TAG:-chk}
 mkdir -p $O
-timeout -k 10 800 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
-  ${PYTEST_ARGS} > $O/pytest_gpu.log 2>&1
-rc=$?
-tail -5 $O/pytest_gpu.log
-[ $rc -eq 0 ] || exit $rc
-[ -n "${NO_BENCH}" ] && exit 0
-timeout -k 10 500 python bench.py ${BENCH_ARGS} > $O/bench.json 2> $O/bench.err || exit $?
-tail -c 1500 $O/bench.json
+timeout -k 10 300 python3 -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu \
+  tests/test_gpu_configs.py -k "folded or resident or dataset_a1 or full_bayes_graph" > $O/pytest_new.log 2>&1 \
+  || { tail -30 $O/pytest_new.log; exit 3; }
+tail -3 $O/pytest_new.log
+timeout -k 10 700 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests \
+  > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 4; }
+tail -3 $O/pytest_gpu.log
+[ -n "$NO_AB" ] || { CONFIGS="2 3 5" REPS=2 STEPS=3000 timeout -k 10 600 bash scripts/ab_variants.sh > $O/ab.log 2>&1 || { tail $O/ab.log; exit 5; }; cat $O/ab.log; }
+[ -n "$NO_BENCH" ] || { timeout -k 10 500 python3 bench.py > $O/bench.json 2> $O/bench.err || { tail $O/bench.err; exit 6; }; tail -c 400 $O/bench.json; }

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-6 SQ counter passes of the step kernels (scripts/gpu_pmc.sh, two passes each): configs 4 / 5
+# SQ counter passes of the step kernels (scripts/gpu_pmc.sh, two passes each): configs 4 / 5
 # at 64 chains per launch (the compute-bound regime) and config 2 / 4 / 5 with one chain.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 R=$PWD
