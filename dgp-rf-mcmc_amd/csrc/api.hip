@@ -262,7 +262,11 @@ int dgprf_plan_init(dgprf_plan_t* pl) {
   pl->rt_per_group = 1;
   pl->rg_full_bayes = 0;
   pl->fold_out = 0;
-  if (pl->n_row_tiles > 16 && !pl->bwd_tiles) {
+  // Many chains per launch (the chip full of chains: throughput, not latency): one row group per
+  // chain, so each chain writes ONE gW partial row per parameter instead of one per row tile and the
+  // update kernel reads one (at 64 chains it streams 13 rows per parameter of every chain)
+  const bool mc_rg = pl->n_chains >= DGPRF_MC_RG_CHAINS && pl->n_row_tiles > 1;
+  if ((pl->n_row_tiles > 16 || mc_rg) && !pl->bwd_tiles) {
     bool ok = true, ok_fb = true;
     dgprf_sk::RgCfg c;
     for (int l = 0; l < L; ++l) {
@@ -270,7 +274,7 @@ int dgprf_plan_init(dgprf_plan_t* pl) {
       ok_fb = ok_fb && dgprf_sk::rg_config(*pl, l, true, c);
     }
     if (ok) {
-      pl->rt_per_group = (pl->n_row_tiles + 15) / 16;
+      pl->rt_per_group = pl->n_row_tiles > 16 ? (pl->n_row_tiles + 15) / 16 : pl->n_row_tiles;
       pl->rg_full_bayes = ok_fb ? 1 : 0;
     }
   }

@@ -42,6 +42,11 @@ constexpr int OST = 68;  // LDS row stride of the staged Omega block (16B-aligne
 // Row stride of the gW partial rows (floats): w_total plus this padding, so the rows a lane of the
 // update kernel reads (configs 4 / 5: w_total x 4 B = 0x320000 / 0x310000 apart) do not share
 // their low address bits
+// Chains per launch from which a plan with <= 16 row tiles takes the row-group backward with one
+// row group per chain (dgprf_plan_init)
+#ifndef DGPRF_MC_RG_CHAINS
+#define DGPRF_MC_RG_CHAINS 16
+#endif
 #ifndef DGPRF_GW_PAD
 #define DGPRF_GW_PAD 0
 #endif
@@ -132,7 +137,15 @@ __device__ __forceinline__ float a0_sum1(const float* p, int sl) { return sl ? p
 // is b % 8; every workgroup of row tile rt gets group rt % 8, so the slice partials it exchanges
 // with the neighbouring layers' kernels stay within one L2.  Speed only: correctness never depends
 // on placement.  Blocks past the last row tile exit at once.
+// rt_per_xcd == 0: a plain row-major map (rt = b / ns) — several chains per launch with fewer than
+// 8 row tiles / groups each, where the XCD map would leave XCDs idle (every chain's blocks start at
+// a multiple of 8).
 __device__ __forceinline__ bool tile_of_block(const LayerK& a, int& rt, int& sl) {
+  if (a.rt_per_xcd == 0) {
+    rt = (int)blockIdx.x / a.ns;
+    sl = (int)blockIdx.x - rt * a.ns;
+    return rt < a.n_rt;
+  }
   const int b = blockIdx.x, grp = b & 7, idx = b >> 3;
   const int j = idx / a.ns;
   sl = idx - j * a.ns;
@@ -624,6 +637,19 @@ __device__ __forceinline__ void w_update_quad(const K& a, const int e0, const in
 // RBF d = 16 layers lost 8 % with 22 spilled).
 constexpr int STEP_WPE = 3;
 
+// (row tile | row group, slice) workgroups of one launch: the XCD-aware map, or the plain map for
+// several chains with fewer than 8 row tiles / groups each (tile_of_block)
+inline void set_block_map(LayerK& a, int n_rt, int n_chains) {
+  a.n_rt = n_rt;
+  if (n_chains > 1 && n_rt < 8) {
+    a.rt_per_xcd = 0;
+    a.main_blocks = n_rt * a.ns;
+  } else {
+    a.rt_per_xcd = (n_rt + 7) / 8;
+    a.main_blocks = 8 * a.rt_per_xcd * a.ns;
+  }
+}
+
 inline LayerK make_layer_k(const dgprf_plan_t& pl, const StepDev& sd, int l, int& lds_floats,
                     bool bwd = false, int nwb = NW) {
   LayerK a;
@@ -676,9 +702,8 @@ inline LayerK make_layer_k(const dgprf_plan_t& pl, const StepDev& sd, int l, int
            (!blk4 || (a.g <= 16 && a.gp <= 16)) && a.R % 4 == 0 && pl.ws_chain < (1 << 29);
   a.xmag = div_magic(dpad);
   a.dmag = div_magic(a.g);
-  a.n_rt = pl.n_row_tiles;
   a.ns = pl.ns[l];
-  a.rt_per_xcd = (pl.n_row_tiles + 7) / 8;
+  set_block_map(a, pl.n_row_tiles, pl.n_chains);
   // full_bayesian=True: z rows, hyper partials, per-wave LDS sums [4][round4(2d+1)]
   a.a0 = (l == 0 && pl.a0_off >= 0 && sd.ws) ? sd.ws + pl.a0_off : nullptr;
   a.z = sd.z ? sd.z + pl.omega_off[l] : nullptr;
@@ -718,7 +743,6 @@ inline LayerK make_layer_k(const dgprf_plan_t& pl, const StepDev& sd, int l, int
       a.wstage = 0;  // no room for the staging next to the slice image: the 4-wave form
     }
   }
-  a.main_blocks = 8 * a.rt_per_xcd * a.ns;
   a.a0_sl = 0;
   if (a.a0 && !sd.bd.A1) {  // the A_1 GEMM's K parts (agemm.hip): two slabs, summed here as slab 0 + slab 1
     const int64_t rows = (pl.batch + 31) / 32 * 32;

@@ -679,9 +679,7 @@ hipError_t launch_step_bwd(const dgprf_plan_t& pl, const StepDev& sd, int layer,
     // row-wave backward (narrow slices after the fused forward): no barrier in the row-tile loop
     int lds_floats = 0;
     LayerK a = make_layer_k(pl, sd, layer, lds_floats, /*bwd=*/true, 4);
-    a.n_rt = pl.n_gw_rows;
-    a.rt_per_xcd = (pl.n_gw_rows + 7) / 8;
-    a.main_blocks = 8 * a.rt_per_xcd * a.ns;
+    set_block_map(a, pl.n_gw_rows, pl.n_chains);
     a.rt_per_rg = pl.rt_per_group;
     a.cmp = 1;
     a.rw_one = a.last;
@@ -714,9 +712,7 @@ hipError_t launch_step_bwd(const dgprf_plan_t& pl, const StepDev& sd, int layer,
     if (!rg_config(pl, layer, sd.full_bayes != 0, c)) return hipErrorInvalidValue;
     int lds_floats = 0;
     LayerK a = make_layer_k(pl, sd, layer, lds_floats, /*bwd=*/true, 4);
-    a.n_rt = pl.n_gw_rows;
-    a.rt_per_xcd = (pl.n_gw_rows + 7) / 8;
-    a.main_blocks = 8 * a.rt_per_xcd * a.ns;
+    set_block_map(a, pl.n_gw_rows, pl.n_chains);
     a.rt_per_rg = pl.rt_per_group;
     a.ncw = c.ncw;
     a.nrw = c.nrw;
