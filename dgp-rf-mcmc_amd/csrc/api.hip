@@ -264,8 +264,14 @@ int dgprf_plan_init(dgprf_plan_t* pl) {
   pl->fold_out = 0;
   // Many chains per launch (the chip full of chains: throughput, not latency): one row group per
   // chain, so each chain writes ONE gW partial row per parameter instead of one per row tile and the
-  // update kernel reads one (at 64 chains it streams 13 rows per parameter of every chain)
-  const bool mc_rg = pl->n_chains >= DGPRF_MC_RG_CHAINS && pl->n_row_tiles > 1;
+  // update kernel reads one (at 64 chains it streams 13 rows per parameter of every chain).  Only
+  // for wide layers (>= 8 slices each): the row tiles of a chain then run in one workgroup per
+  // slice, which a narrow model cannot afford.  B = 200 chain-steps/s at 16 / 64 chains, per-row-
+  // tile -> row group: config 4 14.6k / 14.7k -> 17.8k / 19.8k, config 5 15.2k / 15.3k -> 17.8k /
+  // 18.0k; config 2 (2 slices) 217k / 280k -> 56k / 179k, config 3 (4) 141k / 168k -> 58k / 159k
+  int min_ns = DGPRF_NS_MAX;
+  for (int l = 0; l < L; ++l) min_ns = std::min(min_ns, pl->ns[l]);
+  const bool mc_rg = pl->n_chains >= DGPRF_MC_RG_CHAINS && pl->n_row_tiles > 1 && min_ns >= 8;
   if ((pl->n_row_tiles > 16 || mc_rg) && !pl->bwd_tiles) {
     bool ok = true, ok_fb = true;
     dgprf_sk::RgCfg c;

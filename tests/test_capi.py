@@ -121,18 +121,22 @@ def test_fold_out_plan_choice():
 
 
 def test_many_chain_plans_take_one_row_group_per_chain():
-    """From 16 chains per launch a plan of <= 16 row tiles takes the row-group backward with one row
-    group per chain (dgprf_plan_init): one gW partial row per parameter (n_gw_rows = 1) instead of
-    one per 16-row tile; fewer chains keep the per-row-tile backward."""
+    """From 16 chains per launch a plan of <= 16 row tiles whose layers span >= 8 slices takes the
+    row-group backward with one row group per chain (dgprf_plan_init): one gW partial row per
+    parameter (n_gw_rows = 1) instead of one per 16-row tile; fewer chains, or narrow layers, keep
+    the per-row-tile backward."""
     from dgprf import _native as N
-    mk = lambda C, B=200: N.make_plan(8, 1, [N.RBF] * 3, [1024] * 3, [8, 8, 1], False,
-                                      N.LIK_GAUSSIAN, B, C)
+    mk = lambda C, B=200, n_rf=4096, n_gp=(30, 30, 10): N.make_plan(
+        8, 1, [N.RBF] * 3, [n_rf] * 3, list(n_gp), False, N.LIK_GAUSSIAN, B, C)
     for C in (1, 4, 8):
         p = mk(C)
         assert p.rt_per_group == 1 and p.n_gw_rows == 13
     for C in (16, 64):
         p = mk(C)
+        assert min(p.ns[:3]) >= 8
         assert p.rt_per_group == 13 and p.n_gw_rows == 1 and p.fold_out == 0
+        p = mk(C, n_rf=1024, n_gp=(8, 8, 1))  # 2 slices per layer: per-row-tile backward
+        assert max(p.ns[:3]) < 8 and p.rt_per_group == 1 and p.n_gw_rows == 13
     p = mk(64, B=16)  # one row tile: nothing to group
     assert p.rt_per_group == 1 and p.n_gw_rows == 1
     p = mk(64, B=1000)  # > 16 row tiles: the large-batch row groups (<= 16 partial rows)

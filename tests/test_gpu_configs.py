@@ -116,6 +116,9 @@ def test_multichain_wide_slices_grad(dev, cfg, C):
     want = [max((k + 63) // 64, min(8 if C >= 16 and g <= 16 else 4, (k + 3) // 4))
             for k, g in zip(chunks, c["n_gp"])]
     assert list(mc.layout.cpw[:L]) == want
+    # 16 chains of wide layers (configs 4 / 5): one row group per chain in the backward
+    pl = mc.plan_ws(c["B"])[0]
+    assert (pl.rt_per_group == pl.n_row_tiles > 1) == (C >= 16 and cfg in (4, 5))
     mc.z.copy_(one.z)
     mc.hyp.copy_(one.hyp)
     mc.lik_log_var_source = one.lik_log_var_source
