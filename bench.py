@@ -253,32 +253,45 @@ def bench_config(cfg, dev, rank, world, barrier_sync, max_over_ranks, steps):
                                                * 1e-6) / FP32_MFMA_PEAK, 4)}
     # configs 3 / 5 name 8 chains (on 8 GPUs in the reference): here 8 chains per GPU in one launch
     # sequence of the multi-chain engine (its own slice widths), started from this
-    # chain's state; aggregate chain-steps/s, reported beside the one-chain rate
-    chains8 = None
-    if cfg in (3, 5):
+    # chain's state; aggregate chain-steps/s, reported beside the one-chain rate.  Configs 4 / 5
+    # also at 64 chains per GPU (the throughput regime: one backward row group per chain)
+    def chains_leg(C, reps):
         from dgprf import engine as E
         eng = m._engine
-        me = E.Engine(eng.spec, 8, seed=rank_seed(40 + cfg, rank))
+        me = E.Engine(eng.spec, C, seed=rank_seed(40 + cfg + C, rank))
         me.z.copy_(eng.z)
         me.hyp.copy_(eng.hyp)
-        me.theta.copy_(eng.theta.expand(8, -1))
+        me.theta.copy_(eng.theta.expand(C, -1))
         me.init_moments()
         me.lik_log_var_source = eng.lik_log_var_source
         me.build_omega()
         gph = me.graph(X, Y, c["batch"], n, c["lr"], c["beta"], c["T"], 50)
         gph.launch()
-        reps = 4
+        mpl = me.plan_ws(c["batch"])[0]
+        # the chains share Omega_1, so they share one resident projection: built with the graph,
+        # counted below as one recompute per timed region (its time from the one-chain leg)
+        res = resident and mpl.a0_off >= 0 and me.dataset_a1(X) is not None
         barrier_sync()
         t0 = time.perf_counter()
         for _ in range(reps):
             gph.launch()
         barrier_sync()
-        t8 = max_over_ranks(time.perf_counter() - t0)
-        assert torch.isfinite(me.theta).all(), f"config {cfg} 8-chain run diverged"
-        chains8 = {"chains_per_gpu": 8, "slices_per_layer": list(me.layout.ns[:L]),
-                   "chain_steps_per_s": round(world * 8 * reps * 50 / t8, 1),
-                   "us_per_step_all_chains": round(t8 * 1e6 / (reps * 50), 2)}
+        tc = max_over_ranks(time.perf_counter() - t0)
+        assert torch.isfinite(me.theta).all(), f"config {cfg} {C}-chain run diverged"
+        cs = C * reps * 50
+        t_inc = tc + ((proj_ms or 0.0) * 1e-3 if res else 0.0)
+        ex = cs * (sum(fwd_f) + sum(bwd_f) - (a1_skip if res else 0)) + (proj_fl if res else 0)
+        out = {"chains_per_gpu": C, "slices_per_layer": list(mpl.ns[:L]),
+               "bwd_row_groups_per_chain": int(mpl.n_gw_rows),
+               "chain_steps_per_s": round(world * cs / tc, 1),
+               "us_per_step_all_chains": round(tc * 1e6 / (reps * 50), 2),
+               "chain_steps_per_s_incl_projection": round(world * cs / t_inc, 1) if res else None,
+               "step_mfma_frac": round(ex / t_inc / FP32_MFMA_PEAK, 4)}
         del gph, me
+        torch.cuda.empty_cache()
+        return out
+    chains8 = chains_leg(8, 4) if cfg in (3, 5) else None
+    chains64 = chains_leg(64, 3) if cfg in (4, 5) else None
     # S posterior samples (the chain's W at S successive steps) scored by ONE add_samples call:
     # every sample in one launch of the predictive kernel (grid.z = sample), then the fold; S = the
     # reference driver's default sample count (60), config 5 (1e6 test rows, ~27 ms per sample) 3
@@ -354,7 +367,7 @@ def bench_config(cfg, dev, rank, world, barrier_sync, max_over_ranks, steps):
                               "predictive_kernel_ms_excl_projection": round(k_ms_excl, 3),
                               "s8d_flops_per_sample": int(fp)} if pred_a1_shared else None),
            "a1_gemm": a1,
-           "chains8_per_gpu": chains8}
+           "chains8_per_gpu": chains8, "chains64_per_gpu": chains64}
     del m, acc, X, Y, Xt, Yt
     torch.cuda.empty_cache()
     return out

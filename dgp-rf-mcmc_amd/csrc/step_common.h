@@ -578,15 +578,28 @@ __device__ __forceinline__ void w_update_quad(const K& a, const int e0, const in
   if constexpr (GIN) {
     gr = bload4(make_rsrc(a.grad_in + cw, a.w_total), off);
   } else {
-    // sum the row-tile gW partials in a fixed order: groups of 16 independent loads
+    // sum the row-tile gW partials in a fixed order: groups of 16 independent loads (rows past
+    // n_rt read 0 through the descriptor bound and leave the sum unchanged).  One row (a row group
+    // per chain) or <= 4 rows: only those loads — the 15 / 12 bound-clipped ones still pass
+    // through the texture path (64 chains of config 4 / 5: 3,227 -> 3,188 / 3,542 -> 3,491 us)
     const rsrc_t rs = make_rsrc(a.gwp + (int64_t)chain * a.ws_cs, (int64_t)a.n_rt * a.gw_ld);
     f4 sacc = f4zero();
-    for (int rt0 = 0; rt0 < a.n_rt_pad; rt0 += 16) {
-      f4 v[16];
+    if (a.n_rt == 1) {
+      sacc = bload4(rs, off);
+    } else if (a.n_rt <= 4) {
+      f4 v[4];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) v[j] = bload4(rs, (uint32_t)(((rt0 + j) * a.gw_ld + e0) * 4));
+      for (int j = 0; j < 4; ++j) v[j] = bload4(rs, (uint32_t)((j * a.gw_ld + e0) * 4));
 #pragma unroll
-      for (int j = 0; j < 16; ++j) sacc += v[j];
+      for (int j = 0; j < 4; ++j) sacc += v[j];
+    } else {
+      for (int rt0 = 0; rt0 < a.n_rt_pad; rt0 += 16) {
+        f4 v[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v[j] = bload4(rs, (uint32_t)(((rt0 + j) * a.gw_ld + e0) * 4));
+#pragma unroll
+        for (int j = 0; j < 16; ++j) sacc += v[j];
+      }
     }
     gr = sacc;
   }
