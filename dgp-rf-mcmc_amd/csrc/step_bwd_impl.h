@@ -55,26 +55,26 @@ __device__ __forceinline__ void rcf_stage(const LayerK& a, const float* W, const
 }
 
 // This wave's share of F_L[row lr] = sum_f Phi[lr][f] W_L[f] (layers/rf_layers.py:42-44,
-// layers/GP_weight_layers.py:11-15, g_L = 1): 16-feature chunks wave, wave + 4, ... in order, the A
-// tile on v_mfma_f32_16x16x4_f32 from the staged Omega_L rows and the X tile, features and the W_L
-// dot product as in k_step_fwd's g = 1 body; summed over the lane's 4 features then the 4 feature
-// groups (every lane of row lr ends with the same value).
+// layers/GP_weight_layers.py:11-15, g_L = 1): 16-feature chunks wave, wave + nw, ... in order (nw
+// waves in the workgroup), the A tile on v_mfma_f32_16x16x4_f32 from the staged Omega_L rows and the
+// X tile, features and the W_L dot product as in k_step_fwd's g = 1 body; summed over the lane's 4
+// features then the 4 feature groups (every lane of row lr ends with the same value).
 template <int KS, bool RBF>
 __device__ __forceinline__ float rcf_row_partial(const LayerK& a, const float* smem,
-                                                 const float (&xf)[8], float cl, int wave, int lr,
-                                                 int lq) {
+                                                 const float (&xf)[8], float cl, int wave, int nw,
+                                                 int lr, int lq) {
   const int R = a.R, d = a.d, ost = R + 16, nch = R >> 4;
   const float* wl = smem + a.rcf_off;
   const float* ol = wl + (RBF ? 2 * R : R);
   float acc = 0.f;
-  // four chunks per group (c0, c0 + 4, c0 + 8, c0 + 12: R % 256 == 0, so every wave's chunk count
-  // is a multiple of 4): their A-tile chains are issued together, then the four chunks' features
-  // and dot products — independent dependency chains for one wave per SIMD to overlap
-  for (int c0 = wave; c0 < nch; c0 += 16) {
+  // four chunks per group (c0, c0 + nw, c0 + 2 nw, c0 + 3 nw: R % (64 nw) == 0, so every wave's
+  // chunk count is a multiple of 4): their A-tile chains are issued together, then the four chunks'
+  // features and dot products — independent dependency chains to overlap
+  for (int c0 = wave; c0 < nch; c0 += 4 * nw) {
     f4 at[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int f0 = (c0 + 4 * q) * 16;
+      const int f0 = (c0 + nw * q) * 16;
       at[q] = f4zero();
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
@@ -85,7 +85,7 @@ __device__ __forceinline__ float rcf_row_partial(const LayerK& a, const float* s
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int f0 = (c0 + 4 * q) * 16;
+      const int f0 = (c0 + nw * q) * 16;
       float p0[4], p1[4];
       features<RBF>(at[q], cl, p0, p1);
       const f4 w0 = *reinterpret_cast<const f4*>(wl + f0 + 4 * lq);
@@ -107,9 +107,11 @@ __device__ __forceinline__ float rcf_row_partial(const LayerK& a, const float* s
 // leaves (1 < g): 0 = chosen at run time (g % 16 == 0: transposed tile, 16-byte lanes; else dword
 // stores from the MFMA tile), 1 = transposed tile only, 2 = staged per wave in LDS and stored as
 // contiguous 16-byte lanes only (a.gst_off).
-// RCF: the folded output layer's instance (g = 1, W-only, 4 waves): F_L recomputed here.
+// RCF: the folded output layer's instance (g = 1, W-only, NWB = 4): F_L recomputed here, by 4 or
+// (R % 512 == 0) 8 waves — waves 4-7 join the copy of the layer, the prologue and the recompute, then
+// leave; the rest of the backward is the 4-wave body.
 template <int KS, int NOT, bool RBF, bool G1, bool FB, int NWB, int GSM, bool RCF = false>
-__global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT == 1 && !FB && (KS == 1 || KS == 2 || (KS == 4 && !RBF))) ? STEP_WPE : 1))) void k_step_bwd(const LayerK a) {
+__global__ __launch_bounds__(RCF ? 512 : 64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT == 1 && !FB && (KS == 1 || KS == 2 || (KS == 4 && !RBF))) ? STEP_WPE : 1))) void k_step_bwd(const LayerK a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr bool WST = NWB == 8;  // whole-slice staging (a.wstage == 1 exactly then)
   int rt, sl;
@@ -199,8 +201,10 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
   if (a.fast) {
     // ---- single burst: W/Omega block, X tile, dF (or F_L) partials and Y rows
     f4 sw[2], so;
+    // (an 8-wave RCF workgroup: waves 0-3 stage the block)
+    const bool stager = !RCF || threadIdx.x < 256;
     if (WST && dphi) stage_slice_lds(a, W, om, fb0, smem);
-    if (!WST && dphi) {
+    if (!WST && dphi && stager) {
       const rsrc_t rw = make_rsrc(W, (int64_t)(RBF ? 2 : 1) * R * g);
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
@@ -218,7 +222,7 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
                         [&]() { rcf_stage<RBF>(a, W, om, smem); });
     else
       elem_prologue(a, chain, row0, TR * g, xs, dfs, dfst, ysh, red);
-    if (!WST && dphi) {
+    if (!WST && dphi && stager) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) *reinterpret_cast<f4*>(wsl + 4 * ((int)threadIdx.x + 256 * j)) = sw[j];
       *reinterpret_cast<f4*>(osl + (threadIdx.x >> 4) * OST + 4 * (threadIdx.x & 15)) = so;
@@ -244,16 +248,19 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
     float xr[8];
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) xr[ks] = (ks < KS && 4 * ks < d) ? xs[lr * a.xst + 4 * ks + lq] : 0.f;
-    const float v = rcf_row_partial<KS, RBF>(a, smem, xr, cl, wave, lr, lq);
+    const int nw = (int)(blockDim.x >> 6);
+    const float v = rcf_row_partial<KS, RBF>(a, smem, xr, cl, wave, nw, lr, lq);
     STEP_STAMP(stamp_base, 7);
     if (lq == 0) red[wave * TR + lr] = v;
     __syncthreads();
     STEP_STAMP(stamp_base, 10);
     if (threadIdx.x < TR) {
       const int r = threadIdx.x;
-      const float f = ((red[r] + red[TR + r]) + red[2 * TR + r]) + red[3 * TR + r];
+      float f = red[r];
+      for (int w = 1; w < nw; ++w) f += red[w * TR + r];  // wave order
       dfs[r * dfst] = row0 + r < B ? f : 0.f;
     }
+    if (threadIdx.x >= 256) return;  // waves 4-7 (no later barrier waits for an ended wave)
   }
   // dF_l tile [16][g]: the last layer turns F_L into the likelihood gradient in place;
   // otherwise dF_l = dX_{l+1}[:, :g_l] (already summed above)
@@ -625,6 +632,15 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu((NOT =
 // the 8-wave (whole-slice) instances fix the gW store form at compile time: transposed tile for
 // g % 16 == 0 (and g == 1, which uses neither), LDS-staged otherwise (make_layer_k reserves the
 // staging whenever it keeps the whole-slice layout)
+// the folded output layer's workgroup: 8 waves when R % 512 == 0 (every wave's chunks in groups of
+// 4), 4 otherwise (R % 256 == 0, step_fold_out)
+inline int rcf_threads(const LayerK& a) {
+#ifdef DGPRF_RCF4
+  return 256;
+#else
+  return a.R % 512 == 0 ? 512 : 256;
+#endif
+}
 template <int KS, int NOT, bool G1>
 void k_step_bwd_launch3(bool rbf, bool fb, bool w8, bool t16, dim3 grid, size_t lds,
                         hipStream_t s, const LayerK& a) {
@@ -638,10 +654,10 @@ void k_step_bwd_launch3(bool rbf, bool fb, bool w8, bool t16, dim3 grid, size_t 
     if (a.rcf) {  // folded output layer (make_layer_k sets rcf only for 4-wave W-only launches)
       if (rbf) {
         dgprf::set_lds_limit((const void*)k_step_bwd<KS, NOT, true, G1, false, 4, 0, true>, lds);
-        hipLaunchKernelGGL((k_step_bwd<KS, NOT, true, G1, false, 4, 0, true>), grid, dim3(256), lds, s, a);
+        hipLaunchKernelGGL((k_step_bwd<KS, NOT, true, G1, false, 4, 0, true>), grid, dim3(rcf_threads(a)), lds, s, a);
       } else {
         dgprf::set_lds_limit((const void*)k_step_bwd<KS, NOT, false, G1, false, 4, 0, true>, lds);
-        hipLaunchKernelGGL((k_step_bwd<KS, NOT, false, G1, false, 4, 0, true>), grid, dim3(256), lds, s, a);
+        hipLaunchKernelGGL((k_step_bwd<KS, NOT, false, G1, false, 4, 0, true>), grid, dim3(rcf_threads(a)), lds, s, a);
       }
       return;
     }
