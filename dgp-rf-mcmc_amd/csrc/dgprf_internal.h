@@ -135,7 +135,8 @@ struct ForwardCfg {
   int rows_tt;     // 16-row tiles per row-kernel workgroup (2: tiles outnumber the CUs)
   int64_t chunk, scratch_floats;
 };
-ForwardCfg forward_cfg(const dgprf_plan_t& pl, int64_t n);
+// n_samples: posterior samples scored by one launch (grid.z); the path choice counts all its rows
+ForwardCfg forward_cfg(const dgprf_plan_t& pl, int64_t n, int n_samples = 1);
 hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const float* omega,
                                const float* der, const float* X, const float* Y, int y_cols,
                                int64_t n, float* const* f_out, float* logp, float* se,

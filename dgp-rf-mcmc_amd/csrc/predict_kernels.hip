@@ -1273,7 +1273,7 @@ static int device_cus() {
   return cus;
 }
 
-ForwardCfg forward_cfg(const dgprf_plan_t& pl, int64_t n) {
+ForwardCfg forward_cfg(const dgprf_plan_t& pl, int64_t n, int n_samples) {
   ForwardCfg c;
   // wide first layer (d_1 > 32, e.g. 784 pixels): A_1 = X Omega_1 by the tiled GEMM
   // (k_step_agemm), in row chunks of caller-owned scratch, read by layer 0 instead of a d-long
@@ -1293,7 +1293,7 @@ ForwardCfg forward_cfg(const dgprf_plan_t& pl, int64_t n) {
   // the tile kernel gives each 16-row tile ONE wave through all layers: below FWD_TILE_MIN_ROWS
   // rows it leaves most SIMDs idle, and the row kernel with 16 waves per tile (each a sixteenth
   // of every layer's features, F partials summed in LDS) covers the chip instead
-  constexpr int64_t FWD_TILE_MIN_ROWS = 16384;
+  constexpr int64_t FWD_TILE_MIN_ROWS = 16384, FWD_TILE_MANY_ROWS = 65536;
   const bool few = n < FWD_TILE_MIN_ROWS;
   // layers with g > 16 run the tile kernel at 2 waves per SIMD (its 2-4 output tiles per wave do
   // not fit 4): the 4-wave row kernel is faster at every measured size (config 4: 10k / 20k / 40k
@@ -1308,6 +1308,17 @@ ForwardCfg forward_cfg(const dgprf_plan_t& pl, int64_t n) {
     // small sets: 16 waves per tile while every tile has a CU of its own; past that (config 3:
     // 286 tiles) two 8-wave workgroups share a CU (4,573 rows: 43.1 vs 47.8 us with 16 waves)
     default:
+      // a launch of many rows in all — n rows x the samples (grid.z) x the chains (grid.y) of one
+      // launch — fills the chip with one-wave tiles however few rows one sample has, and the tile
+      // kernel's per-tile work is the cheaper one there (config 3, 4,573 rows, 60 samples: 15.9 vs
+      // 21.7 us per sample; config 4, 10,000 rows with g = 30: 289 vs 385 us; the row kernels win
+      // below about 40k-70k rows in all: config 3 x 8 samples 22.4 vs 24.0 us, config 4 x 2 samples
+      // 424 vs 494 us)
+      if ((int64_t)n * n_samples * pl.n_chains >= FWD_TILE_MANY_ROWS) {
+        c.tiles = tile_ok;
+        c.rows_waves = 4;
+        break;
+      }
       c.tiles = tile_ok && !few && !wide_g;
       c.rows_waves = few && small ? ((n + TR - 1) / TR > device_cus() ? 8 : 16) : 4;
       break;
@@ -1349,7 +1360,7 @@ hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const
     smalld = smalld && pl.d[l] <= 32;
     notmax = max(notmax, (pl.n_gp[l] + 15) >> 4);
   }
-  const ForwardCfg cfg = forward_cfg(pl, n);
+  const ForwardCfg cfg = forward_cfg(pl, n, n_samples);
   const bool wide0 = cfg.wide0, tiles = cfg.tiles;
   // a caller-resident A_1 of every row: one chunk, no GEMM
   const bool res = wide0 && a1_full;

@@ -273,6 +273,58 @@ def test_config_predictive_samples_one_launch_bit_equal(dev, cfg, n_test):
     assert np.max(np.abs(got - ref)) < 2e-5 * max(1.0, np.max(np.abs(ref))), cfg
 
 
+@pytest.mark.parametrize("cfg,n_test", [(3, 1001), (4, 960)])
+def test_predictive_many_samples_take_tiles(dev, cfg, n_test):
+    """One launch scoring S samples of n rows with n S >= 65,536 (forward_cfg counts every row of
+    the launch) takes the tile kernel although one sample's rows are below its threshold (config
+    3) or its layers have g > 16 (config 4, whose one-sample launches keep the row kernel): the
+    log-sum-exp accumulators agree with the 4-wave row kernel's (FWD_ROWS pinned) to fp32
+    rounding, and for config 3 with the oracle's log-sum-exp of the S samples per row."""
+    from dgprf import _native as N
+    from dgprf import engine as E
+    from dgprf.engine import ops
+    c = CONFIGS[cfg]
+    m, p = _model(c, 70 + cfg)
+    eng = m._engine
+    Xt, Yt = _data(c, n_test, 400 + cfg)
+    Xd = torch.tensor(Xt, dtype=torch.float32, device=dev)
+    Yd = torch.tensor(Yt, dtype=torch.float32, device=dev)
+    E.set_seed(71)
+    S = 70
+    assert n_test * S >= 65536
+    thetas = torch.stack([E.normal((1, eng.layout.w_total), N.RNG_W) for _ in range(S)])
+    eng.build_omega()
+    a1 = eng.dataset_a1(Xd)
+    gauss = c["lik"] == "gaussian"
+
+    def lse():
+        scr = eng.forward_scratch(n_test, S)
+        acc = [torch.full((1, n_test), -np.inf, device=dev), torch.zeros(1, n_test, device=dev),
+               torch.zeros(1, n_test, device=dev) if gauss else None]
+        ops().forward_samples(eng._plan_t(eng.layout), thetas, eng.omega, eng.der, Xd, a1, Yd,
+                              acc[0], acc[1], acc[2], scr)
+        torch.cuda.synchronize()
+        return cpu(acc[0])[0] + np.log(cpu(acc[1])[0])
+
+    got = lse()
+    eng.set_forward_path(N.FWD_ROWS)
+    rows = lse()
+    eng.set_forward_path(N.FWD_AUTO)
+    assert np.all(np.isfinite(got))
+    assert np.max(np.abs(got - rows)) < 2e-5 * max(1.0, np.max(np.abs(rows))), cfg
+    if cfg == 3:
+        lps = []
+        for j in range(S):
+            W = unpack(eng, thetas[j])
+            pj = O.Params(p.d_in, p.d_out, p.n_rf, p.n_gp, p.kinds, p.likelihood, False, z=p.z,
+                          W=W, log_inv_ls=p.log_inv_ls, lik_log_var=p.lik_log_var)
+            lps.append(O.log_prob(pj, O.forward(pj, Xt), Yt))
+        lps = np.stack(lps)
+        mx = lps.max(axis=0)
+        ref = mx + np.log(np.exp(lps - mx).sum(axis=0))
+        assert np.max(np.abs(got - ref)) < 2e-5 * max(1.0, np.max(np.abs(ref)))
+
+
 @pytest.mark.parametrize("cfg", [3, 4, 5])
 def test_config_graph_steps_finite_and_deterministic(dev, cfg):
     """200 graph-replayed steps with on-device minibatches of B = 200 at the config's N (config 5
