@@ -132,7 +132,7 @@ hipError_t launch_fresh_omega(const dgprf_plan_t& pl, const StepDev& sd, hipStre
 struct ForwardCfg {
   bool wide0, tiles;
   int rows_waves;  // waves per workgroup of the row kernel (4, 8 or 16)
-  int rows_tt;     // 16-row tiles per row-kernel workgroup (2: tiles outnumber the CUs)
+  int rows_tt;     // 16-row tiles per row-kernel workgroup (2: one sample, tiles outnumber the CUs)
   int64_t chunk, scratch_floats;
 };
 // n_samples: posterior samples scored by one launch (grid.z); the path choice counts all its rows
@@ -141,8 +141,11 @@ hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const
                                const float* der, const float* X, const float* Y, int y_cols,
                                int64_t n, float* const* f_out, float* logp, float* se,
                                float* lse_m, float* lse_s, float* se_sum, float* scratch,
-                               hipStream_t s, const float* a1_full = nullptr, int n_samples = 1);
-// (a1_full: X Omega_1 of all n rows, precomputed by the caller for a wide first layer: no A_1 GEMM)
+                               hipStream_t s, const float* a1_full = nullptr, int n_samples = 1,
+                               int path_samples = 0);
+// (a1_full: X Omega_1 of all n rows, precomputed by the caller for a wide first layer: no A_1 GEMM;
+// path_samples > 0: choose the kernel as for a launch of that many samples — the per-sample
+// launches of a multi-sample call take the kernel its one-launch form takes, so both agree bitwise)
 // Posterior-predictive LSE fold of n_samples samples of every chain (thetas [n_samples][C][w_total]),
 // sample order: two samples per pass of the pair kernel for lean models (layer 0 shared) — every
 // pair in one launch when scratch holds forward_samples_scratch floats — else one
@@ -152,7 +155,7 @@ hipError_t launch_forward_samples(const dgprf_plan_t& pl, const float* thetas, i
                                   const float* A1, const float* Y, int y_cols, int64_t n, float* lse_m,
                                   float* lse_s, float* se_sum, float* scratch,
                                   int64_t scratch_floats, hipStream_t s);
-bool forward_pairs_ok(const dgprf_plan_t& pl, int64_t n);
+bool forward_pairs_ok(const dgprf_plan_t& pl, int64_t n, int n_samples = 1);
 // scratch floats that let launch_forward_samples run every pair in one launch (0: not applicable)
 int64_t forward_samples_scratch(const dgprf_plan_t& pl, int64_t n, int n_samples);
 hipError_t launch_lse_finalize(const float* lse_m, const float* lse_s, const float* se_sum,

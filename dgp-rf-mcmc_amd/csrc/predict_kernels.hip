@@ -1323,11 +1323,13 @@ ForwardCfg forward_cfg(const dgprf_plan_t& pl, int64_t n, int n_samples) {
       c.rows_waves = few && small ? ((n + TR - 1) / TR > device_cus() ? 8 : 16) : 4;
       break;
   }
-  // past one tile per CU a CU runs two tiles anyway: one 16-wave workgroup over two tiles fetches
-  // each W / Omega fragment once for both (instead of two 8-wave workgroups fetching the model
-  // twice).  DGPRF_FWD_ROWS8 keeps the two-workgroup form.
+  // past one tile per CU a CU runs two tiles anyway: for ONE sample of one chain, one 16-wave
+  // workgroup over two tiles fetches each W / Omega fragment once for both (instead of two 8-wave
+  // workgroups fetching the model twice): config 3's 4,573 rows 36.4 vs 40.0 us.  A launch of
+  // several samples or chains keeps the 8-wave workgroups (2 / 4 samples: 30.3 vs 35.8 / 23.7 vs
+  // 26.6 us per sample).  DGPRF_FWD_ROWS8 keeps the two-workgroup form.
   c.rows_tt = 1;
-  if (pl.fwd_path == DGPRF_FWD_AUTO && c.rows_waves == 8 && !c.wide0) {
+  if (pl.fwd_path == DGPRF_FWD_AUTO && c.rows_waves == 8 && !c.wide0 && n_samples * pl.n_chains == 1) {
     c.rows_waves = 16;
     c.rows_tt = 2;
   }
@@ -1347,7 +1349,8 @@ hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const
                                const float* der, const float* X, const float* Y, int y_cols,
                                int64_t n, float* const* f_out, float* logp, float* se,
                                float* lse_m, float* lse_s, float* se_sum, float* scratch,
-                               hipStream_t s, const float* a1_full, int n_samples) {
+                               hipStream_t s, const float* a1_full, int n_samples,
+                               int path_samples) {
   if (n <= 0) return hipSuccess;
   // n_samples > 1: theta holds that many samples ([n_samples][C][w_total]), one per grid.z, and
   // logp / se receive [n_samples][C][n] (no in-kernel fold: the caller folds in sample order)
@@ -1360,7 +1363,7 @@ hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const
     smalld = smalld && pl.d[l] <= 32;
     notmax = max(notmax, (pl.n_gp[l] + 15) >> 4);
   }
-  const ForwardCfg cfg = forward_cfg(pl, n, n_samples);
+  const ForwardCfg cfg = forward_cfg(pl, n, path_samples > 0 ? path_samples : n_samples);
   const bool wide0 = cfg.wide0, tiles = cfg.tiles;
   // a caller-resident A_1 of every row: one chunk, no GEMM
   const bool res = wide0 && a1_full;
@@ -1462,8 +1465,8 @@ hipError_t launch_forward_rows(const dgprf_plan_t& pl, const float* theta, const
 }
 
 // The pair kernel applies where the one-sample path would run the lean tile instance.
-bool forward_pairs_ok(const dgprf_plan_t& pl, int64_t n) {
-  const ForwardCfg cfg = forward_cfg(pl, n);
+bool forward_pairs_ok(const dgprf_plan_t& pl, int64_t n, int n_samples) {
+  const ForwardCfg cfg = forward_cfg(pl, n, n_samples);
   if (!cfg.tiles || cfg.wide0 || TILE_TPW_DEFAULT != 1) return false;
   for (int l = 0; l < pl.n_layers; ++l)
     if (pl.n_gp[l] > 8 || pl.d[l] > 8) return false;
@@ -1479,7 +1482,7 @@ hipError_t launch_forward_samples(const dgprf_plan_t& pl, const float* thetas, i
   // 32-bit buffer offsets across two samples' W
   const bool off_ok = ((int64_t)pl.n_chains * pl.w_total + 2 * (int64_t)pl.n_rf[0] * pl.n_gp[0]) * 4 <
                       ((int64_t)1 << 31);
-  if (!off_ok || !forward_pairs_ok(pl, n)) {
+  if (!off_ok || !forward_pairs_ok(pl, n, n_samples)) {
     const int64_t cn = (int64_t)pl.n_chains * n;
     const int64_t need = forward_samples_scratch(pl, n, n_samples);
     if (need > 0 && scratch && scratch_floats >= need && (A1 || !forward_cfg(pl, n).wide0)) {
@@ -1498,7 +1501,8 @@ hipError_t launch_forward_samples(const dgprf_plan_t& pl, const float* thetas, i
     for (int j = 0; j < n_samples; ++j) {  // one launch per sample (sample order)
       const hipError_t e = launch_forward_rows(pl, thetas + (int64_t)j * pl.n_chains * pl.w_total,
                                                omega, der, X, Y, y_cols, n, nullptr, nullptr,
-                                               nullptr, lse_m, lse_s, se_sum, scratch, s, A1);
+                                               nullptr, lse_m, lse_s, se_sum, scratch, s, A1, 1,
+                                               n_samples);  // the one-launch form's kernel
       if (e != hipSuccess) return e;
     }
     return hipSuccess;
@@ -1540,7 +1544,7 @@ hipError_t launch_forward_samples(const dgprf_plan_t& pl, const float* thetas, i
 int64_t forward_samples_scratch(const dgprf_plan_t& pl, int64_t n, int n_samples) {
   if (n <= 0) return 0;
   const int64_t per = (int64_t)pl.n_chains * n * (pl.likelihood == DGPRF_LIK_GAUSSIAN ? 2 : 1);
-  if (forward_pairs_ok(pl, n)) return n_samples >= 3 ? n_samples * per : 0;
+  if (forward_pairs_ok(pl, n, n_samples)) return n_samples >= 3 ? n_samples * per : 0;
   // one-sample kernels: all samples in one launch (launch_forward_samples takes that form unless
   // a wide first layer's A_1 would come in scratch chunks, i.e. without a resident projection)
   return n_samples >= 2 ? n_samples * per : 0;

@@ -161,10 +161,10 @@ def test_predictive_paths_small_test_set(dev, path, cfg):
 
 @pytest.mark.parametrize("cfg,n", [(3, 4573), (2, 5001)])
 def test_predictive_two_tile_rows(dev, cfg, n):
-    """The default path once the 16-row tiles outnumber the CUs (config 3's 4,573 test rows: 286
-    tiles): the row kernel with two tiles per 16-wave workgroup (forward_cfg rows_tt = 2), whose
-    last workgroup holds a ragged tile (and for 5,001 rows an empty one); per-row log p against the
-    oracle, and identical to the one-tile 8-wave workgroups to fp32 rounding."""
+    """The default path of one sample once the 16-row tiles outnumber the CUs (config 3's 4,573
+    test rows: 286 tiles): the row kernel with two tiles per 16-wave workgroup (forward_cfg rows_tt
+    = 2), whose last workgroup holds a ragged tile (and for 5,001 rows an empty one); per-row log p
+    against the oracle, and equal to the one-tile 8-wave and 16-wave workgroups to fp32 rounding."""
     from dgprf import _native as N
     c = CONFIGS[cfg]
     m, p = _model(c, 35)
@@ -175,6 +175,9 @@ def test_predictive_two_tile_rows(dev, cfg, n):
     m._engine.set_forward_path(N.FWD_ROWS8)
     lp8 = cpu(m._engine.forward(Xt, Yt, logp=True)["logp"][0])
     assert np.max(np.abs(lp - lp8)) < 2e-5 * max(1.0, np.max(np.abs(ref)))
+    m._engine.set_forward_path(N.FWD_ROWS16)
+    lp16 = cpu(m._engine.forward(Xt, Yt, logp=True)["logp"][0])
+    assert np.max(np.abs(lp - lp16)) < 2e-5 * max(1.0, np.max(np.abs(ref)))
 
 
 def test_predictive_multi_round_rows(dev):
